@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Benchmark: decoded+triangulated camera px/s (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+A step is one pass of the fused hot path over one batch of synthetic views
+resident in HBM: k_stats (histogram/threshold pre-pass) + k_decode (Gray decode,
+mask, Gray->binary, ray/plane triangulation, ordered compaction), producing
+what the reference's gray_decode + reconstruct_point_cloud return: col_map,
+row_map, mask and the (xyz, BGR) cloud.  Default workload = BASELINE config 2:
+one 3840x2160 view, 11+11-bit column+row Gray code with inverses (46 planes),
+per GPU per step.  Multi-GPU: weak scaling, views sharded over ranks with no
+data-path collective; the RCCL gather of the clouds to rank 0 is timed
+separately ("gather_ms").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from structured_light_for_3d_model_replication_amd import core, parallel, synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (H, W, Wp, Hp, rows, views per GPU per step)
+    "c1": (720, 1280, 1024, 768, False, 1),
+    "c2": (2160, 3840, 1920, 1080, True, 1),
+    "c3": (1080, 1920, 1920, 1080, True, 36),
+    "c4": (3000, 4000, 1920, 1080, True, 4),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--views", type=int, default=None, help="views per GPU per step (default per config)")
+    ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
+    ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per k_decode launch (from profiles/)")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(H, W, n_planes, n_points, maps=True):
+    """H*W*(2+2(nc+nr)) stack + 3*H*W texture + 15*N_out,
+    + 8*H*W col/row int32 + H*W mask bytes when the maps are written."""
+    px = H * W
+    b = n_planes * px + 3 * px + 15 * n_points
+    if maps:
+        b += 9 * px
+    return b
+
+
+def cpu_baseline(stack_h, tex_h, calib, budget_s):
+    """Time the oracle (NumPy restatement of the reference path, 1 thread)."""
+    from oracle import sl_oracle
+    imgs = list(stack_h)
+    px = stack_h.shape[1] * stack_h.shape[2]
+    n, t0 = 0, time.perf_counter()
+    while True:
+        sl_oracle.decode_triangulate(imgs, tex_h, calib)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or el / n * (n + 1) > 1.5 * budget_s:
+            break
+    return n * px / el, n, el
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    H, W, Wp, Hp, rows, vdef = CONFIGS[a.config]
+    V = a.views or vdef
+    rig = synth.Rig(H=H, W=W, Wp=Wp, Hp=Hp)
+    calib = synth.make_calibration(rig, with_Nc=False)
+    cfg_idx = int(a.config[1:])
+    stacks, texes = [], []
+    for v in range(V):
+        gv = rank * V + v
+        s, t = synth.render_stack(rig, seed=1000 * cfg_idx + gv, include_rows=rows,
+                                  view_deg=10.0 * gv, device=dev)
+        stacks.append(s)
+        texes.append(t)
+    stack = torch.stack(stacks) if V > 1 else stacks[0][None]
+    tex = torch.stack(texes) if V > 1 else texes[0][None]
+    del stacks, texes
+    n_planes = stack.shape[1]
+    eng = core.Reconstructor(dev)
+    eng.set_calibration(calib, H, W)
+    eng.reserve(V, H * W)
+    n_cols, n_rows = Wp, (Hp if rows else 1080)
+    out = {}
+
+    def step(o, maps=True):
+        return eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
+                                      xyz_dtype=torch.float32, out=o)
+
+    for _ in range(a.warmup):
+        step(out)
+    eng.sync()
+    n_pts = int(out["view_offsets"][-1].item())
+    eng.profile_enable(a.steps)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(out)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    stats_ms, decode_ms, nl = eng.profile_read()
+    eng.sync()
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+
+    # secondary: cloud-only mode (what generate_cloud runs: row planes unread)
+    out2 = {}
+    for _ in range(2):
+        step(out2, maps=False)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    for _ in range(a.steps):
+        step(out2, maps=False)
+    torch.cuda.synchronize(dev)
+    el_cloud = time.perf_counter() - t1
+
+    gather_ms = None
+    if world > 1:
+        n_loc = int(out["view_offsets"][-1].item())
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        tg = time.perf_counter()
+        parallel.gather_cloud(out["xyz"][:n_loc], out["bgr"][:n_loc], dst=0)
+        torch.cuda.synchronize(dev)
+        gt = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=dev)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        gather_ms = 1e3 * float(gt.item())
+
+    if rank == 0:
+        px_step = V * H * W
+        value = world * px_step * a.steps / el
+        dec_avg_ms = decode_ms / max(nl, 1)
+        ab = algorithmic_bytes(H, W, n_planes, n_pts / V, maps=True) * V
+        achieved = ab / (dec_avg_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(a.traffic):
+            try:
+                tj = json.load(open(a.traffic))
+                if tj.get("config") == a.config and tj.get("views") == V:
+                    traffic = tj.get("bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        cpu = None
+        if a.cpu_baseline and world == 1:
+            one_view = stack[0].cpu().numpy()
+            one_tex = tex[0].cpu().numpy()
+            v_cpu, n_cpu, el_cpu = cpu_baseline(one_view, one_tex, calib, a.cpu_seconds)
+            cpu = {"value": v_cpu, "unit": "px/s", "cores": 1, "kind": "port",
+                   "sample": f"{n_cpu} x {W}x{H} view(s), {n_planes} planes, oracle/sl_oracle.py "
+                             f"(NumPy restatement, bit-exact to reference fixtures), 1 thread, {el_cpu:.1f} s"}
+        res = {
+            "metric": "decoded+triangulated px/s",
+            "value": value,
+            "unit": "px/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": 1e3 * el / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"BASELINE config {cfg_idx}: {V} x {W}x{H} view(s) per GPU per step, "
+                                   f"{n_planes} planes (Gray {'11+11' if rows else str(n_planes // 2 - 1) + '+0'}"
+                                   f" bits + inverses), outputs col/row/mask maps + fp32 xyz/BGR cloud",
+                       "views_per_gpu": V, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
+                       "parallelism": f"views sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_decode", "kernel_avg_ms": dec_avg_ms,
+                         "algorithmic_bytes_per_launch": ab},
+            "cpu_baseline": cpu,
+            "k_stats_avg_ms": stats_ms / max(nl, 1),
+            "points_per_view": n_pts / V,
+            "cloud_only_px_per_s": world * px_step * a.steps / el_cloud,
+            "gather_ms": gather_ms,
+        }
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+/*
+ * slgpu.h -- C ABI of libslgpu.so, the MI355X (gfx950) implementation of the
+ * structured-light reconstruction hot path of
+ * Nuttoty/Structured_Light_for_3D_Model_Replication:
+ *
+ *   gray_decode(folder, n_cols, n_rows)          server/sl_system.py:508-580
+ *   reconstruct_point_cloud(col, row, mask, tex, calib)  server/sl_system.py:584-653
+ *   generate_cloud(scan_dir, calib_file)         server/sl_system.py:483-694
+ *
+ * The reference has no FFI; its boundary is the Python function triple above
+ * (called from server/gui.py:563, multi_point_cloud_process.py:206-212 and
+ * Old/process_cloud.py:231-233).  This header is what a ctypes binding of that
+ * triple calls; see INTEGRATION.md for the binding.
+ *
+ * Conventions
+ *  - Every entry point returns SL_OK (0) or a negative SL_E* code; the message
+ *    of the last failure on a context is sl_ctx_last_error().
+ *  - Pointers named "device" are HIP device pointers owned by the caller.  The
+ *    library owns only the calibration tables and scratch inside a context.
+ *  - A context belongs to one device; calls on one context must be serialised
+ *    by the caller (one context per thread or per device).  There is no global
+ *    state, so independent contexts may be used concurrently.
+ *  - Work is enqueued on `stream` (a hipStream_t; NULL = default stream) and is
+ *    asynchronous unless the function says otherwise.
+ */
+#ifndef SLGPU_H
+#define SLGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SL_ABI_VERSION 1
+
+#define SL_OK 0
+#define SL_EINVAL (-1)    /* bad argument -> Python ValueError                          */
+#define SL_EINDEX (-2)    /* dangling odd image reached: the IndexError of
+                             sl_system.py:553-554                                      */
+#define SL_EHIP (-3)      /* HIP runtime failure -> RuntimeError                        */
+#define SL_ENOCALIB (-4)  /* sl_set_calib not called / shape mismatch -> ValueError       */
+#define SL_ETIMEOUT (-5)  /* a device-side bounded wait expired -> RuntimeError         */
+#define SL_ECAPACITY (-6) /* output capacity smaller than the pixel count -> ValueError   */
+
+/* mask_mode */
+#define SL_MASK_ADAPTIVE 0 /* white > 1.5*pct95(black) & contrast > 0.05*max(contrast):
+                              sl_system.py:526-535                                      */
+#define SL_MASK_FIXED 1    /* white > 40 & contrast > 10:
+                              multi_point_cloud_process.py:36-38, Old/process_cloud.py:47-49 */
+
+/* xyz_dtype */
+#define SL_XYZ_F32 0 /* 12 B/point, the round-to-nearest fp32 of the reference's f64   */
+#define SL_XYZ_F64 1 /* 24 B/point, bit-identical to the reference's f64              */
+
+typedef struct sl_ctx sl_ctx;
+
+int sl_abi_version(void);
+
+/* Create a context on HIP device `device`.  Replaces nothing in the reference
+ * (which keeps no state); the context holds the calibration tables. */
+int sl_ctx_create(int device, sl_ctx** out);
+void sl_ctx_destroy(sl_ctx* ctx);
+const char* sl_ctx_last_error(const sl_ctx* ctx);
+
+/* Pre-size the context's scratch for up to `max_views` views of `max_px`
+ * pixels each so that later calls allocate nothing (required before stream
+ * capture into a hipGraph).  Calls grow scratch on demand otherwise. */
+int sl_ctx_reserve(sl_ctx* ctx, int64_t max_views, int64_t max_px);
+
+/* Upload calibration for an H x W camera (the calib.mat fields loaded at
+ * sl_system.py:493-504).  Host pointers:
+ *   cam_K   3x3 row-major f64            (calib["cam_K"])
+ *   Oc      3 f64                         (calib["Oc"], zeros from calibrate_final)
+ *   planes  Wp x 4 row-major f64 (n0,n1,n2,d) (calib["wPlaneCol"] transposed as at
+ *           sl_system.py:591)
+ *   Nc      3 x (H*W) row-major f64, or NULL (calib["Nc"]).  When Nc equals the
+ *           pinhole rays of cam_K bit for bit (always, for calibrate_final output)
+ *           it is not uploaded and rays are recomputed on the fly; otherwise it
+ *           is kept on the device and read per pixel, as sl_system.py:605-606. */
+int sl_set_calib(sl_ctx* ctx, int H, int W, const double* cam_K, const double* Oc,
+                 const double* planes, int Wp, const double* Nc);
+
+/* Fused gray_decode + reconstruct_point_cloud over `n_views` views.
+ *
+ * stack      device, view v at stack + v*stack_view_stride: n_img planes of H*W
+ *            uint8 in the reference's sorted-file order [white, black, (pattern,
+ *            inverse) x bits...] (sl_system.py:510-520, 553-557).
+ * n_cols/n_rows  projector stripes; ceil(log2()) gives the bit counts exactly as
+ *            sl_system.py:538-539 (each must be in [1, 65536]).
+ * tex_bgr    device, [H][W][3] BGR per view (the colour imread of file 0,
+ *            sl_system.py:580), or NULL to use the white plane replicated.
+ * poses      device, n_views x 4x4 row-major f64 applied to every point of the
+ *            view (turntable merge epilogue), or NULL.
+ * col_out, row_out  device int32 [n_views][H][W], full frame, unmasked (may be
+ *            NULL).  mask_out device uint8 (0/1) [n_views][H][W] (may be NULL).
+ * xyz_out    device, out_capacity x 3 of f32 or f64 (xyz_dtype), NULL for
+ *            decode only.  bgr_out device uint8 out_capacity x 3 (NULL allowed
+ *            only together with xyz_out).  Both 16-byte aligned.
+ * view_offsets  device int64 [n_views+1]: points of view v occupy
+ *            [view_offsets[v], view_offsets[v+1]) of the merged cloud, in
+ *            ascending pixel order inside each view (np.where order,
+ *            sl_system.py:601).  Required when xyz_out is given.
+ * out_capacity  must be >= n_views*H*W.
+ *
+ * Row planes are read only if row_out is non-NULL (the cloud does not use the
+ * row code: sl_system.py:584-653 reads only col_map).
+ * Returns SL_EINDEX / SL_EINVAL for the stack lengths on which the reference
+ * raises IndexError / ValueError. */
+int sl_decode_triangulate(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_stride,
+                          int n_views, int n_img, int H, int W, int n_cols, int n_rows,
+                          const uint8_t* tex_bgr, int64_t tex_view_stride, int mask_mode,
+                          const double* poses, int32_t* col_out, int32_t* row_out,
+                          uint8_t* mask_out, void* xyz_out, int xyz_dtype, uint8_t* bgr_out,
+                          int64_t out_capacity, int64_t* view_offsets, void* stream);
+
+/* reconstruct_point_cloud on caller-supplied maps (sl_system.py:584-653).
+ * col_map device int32 [n_views][H][W]; mask device uint8 [n_views][H][W]
+ * (non-zero = valid); tex_bgr device [n_views][H][W][3].  Outputs as above. */
+int sl_triangulate_maps(sl_ctx* ctx, const int32_t* col_map, const uint8_t* mask,
+                        const uint8_t* tex_bgr, int n_views, int H, int W,
+                        const double* poses, void* xyz_out, int xyz_dtype, uint8_t* bgr_out,
+                        int64_t out_capacity, int64_t* view_offsets, void* stream);
+
+/* Synchronise `stream` and report device-side failures (SL_ETIMEOUT) of the
+ * work enqueued so far on this context.  Blocking. */
+int sl_sync(sl_ctx* ctx, void* stream);
+
+/* Adaptive-mask diagnostics of the last sl_decode_triangulate (blocking):
+ * noise_floor = np.percentile(black, 95) and dynamic_range = max(white-black)
+ * as float32 (sl_system.py:527-528), and the integer thresholds the kernel
+ * compared against (white > thr_white, contrast > thr_contrast). */
+int sl_last_thresholds(sl_ctx* ctx, int view, float* noise_floor, float* dynamic_range,
+                       int* thr_white, int* thr_contrast);
+
+/* Timing: with max_launches > 0, each later launch (up to that many) records
+ * HIP events on its stream around k_stats and around k_decode.  0 disables. */
+int sl_profile_enable(sl_ctx* ctx, int max_launches);
+
+/* Blocking: summed event time (ms) of k_stats and k_decode over the recorded
+ * launches since the last read, and their count; then restarts recording. */
+int sl_profile_read(sl_ctx* ctx, double* stats_ms, double* decode_ms, int* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLGPU_H */

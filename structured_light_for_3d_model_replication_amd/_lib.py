@@ -1,0 +1,93 @@
+"""ctypes binding of libslgpu.so (include/slgpu.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()``.  There is no
+fallback: if the library is missing or has no device, every product entry point
+raises instead of silently computing on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libslgpu.so")
+
+SL_OK = 0
+SL_EINVAL = -1
+SL_EINDEX = -2
+SL_EHIP = -3
+SL_ENOCALIB = -4
+SL_ETIMEOUT = -5
+SL_ECAPACITY = -6
+
+SL_MASK_ADAPTIVE = 0
+SL_MASK_FIXED = 1
+SL_XYZ_F32 = 0
+SL_XYZ_F64 = 1
+
+# every symbol include/slgpu.h declares
+EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_error", "sl_ctx_reserve",
+           "sl_set_calib", "sl_decode_triangulate", "sl_triangulate_maps", "sl_sync",
+           "sl_last_thresholds", "sl_profile_enable", "sl_profile_read")
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int
+_i64 = ctypes.c_int64
+_SIGS = {
+    "sl_abi_version": (_i32, []),
+    "sl_ctx_create": (_i32, [_i32, ctypes.POINTER(_vp)]),
+    "sl_ctx_destroy": (None, [_vp]),
+    "sl_ctx_last_error": (ctypes.c_char_p, [_vp]),
+    "sl_ctx_reserve": (_i32, [_vp, _i64, _i64]),
+    "sl_set_calib": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp]),
+    "sl_decode_triangulate": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32,
+                                     _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp]),
+    "sl_triangulate_maps": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i64, _vp,
+                                   _vp]),
+    "sl_sync": (_i32, [_vp, _vp]),
+    "sl_last_thresholds": (_i32, [_vp, _i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                                  ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "sl_profile_enable": (_i32, [_vp, _i32]),
+    "sl_profile_read": (_i32, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(_i32)]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libslgpu.so (raises RuntimeError if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import "
+                                   f"__graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+class SLError(RuntimeError):
+    pass
+
+
+def check(code: int, ctx=None, what: str = "") -> None:
+    """Map an SL_E* status to the exception type the reference raises."""
+    if code == SL_OK:
+        return
+    msg = what
+    if ctx is not None:
+        raw = load().sl_ctx_last_error(ctx)
+        msg = raw.decode() if raw else what
+    if code in (SL_EINVAL, SL_ENOCALIB, SL_ECAPACITY):
+        raise ValueError(msg)
+    if code == SL_EINDEX:
+        raise IndexError(msg)
+    raise SLError(f"libslgpu error {code}: {msg}")

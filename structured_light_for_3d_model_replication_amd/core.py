@@ -1,0 +1,273 @@
+"""Device-side reconstruction engine: one ``Reconstructor`` per GPU.
+
+Wraps a ``sl_ctx`` of libslgpu.so (include/slgpu.h).  Inputs and outputs are
+torch tensors resident on the GPU; torch supplies device memory and streams
+only -- all arithmetic runs in the hand-written HIP kernels.
+
+Reference correspondence (Nuttoty/Structured_Light_for_3D_Model_Replication):
+``decode_triangulate`` = ``gray_decode`` (server/sl_system.py:508-580) fused
+with ``reconstruct_point_cloud`` (server/sl_system.py:584-653);
+``triangulate_maps`` = ``reconstruct_point_cloud`` on given maps.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+
+MASK_MODES = {"adaptive": _lib.SL_MASK_ADAPTIVE, "fixed": _lib.SL_MASK_FIXED}
+
+
+def _ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _f64c(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+@dataclass
+class Cloud:
+    """Merged cloud of a batch of views on the device.
+
+    ``xyz`` [capacity, 3] (float32 or float64), ``bgr`` [capacity, 3] uint8 and
+    ``view_offsets`` int64 [V+1]; points of view v are rows
+    ``view_offsets[v]:view_offsets[v+1]`` (ascending pixel order).
+    """
+    xyz: torch.Tensor
+    bgr: torch.Tensor
+    view_offsets: torch.Tensor
+
+    def offsets(self) -> np.ndarray:
+        return self.view_offsets.cpu().numpy()
+
+    def view(self, v: int):
+        o = self.offsets()
+        return self.xyz[o[v]:o[v + 1]], self.bgr[o[v]:o[v + 1]]
+
+    def total(self) -> int:
+        return int(self.view_offsets[-1].item())
+
+
+def calibration_arrays(calib: dict, H: int, W: int):
+    """(cam_K 3x3, Oc 3, planes Wp x 4, Nc 3 x HW or None) from a calib dict
+    with the keys loaded at sl_system.py:498-504.  ``wPlaneCol`` is transposed
+    when stored 4 x Wp (sl_system.py:591); ``Nc`` is used only when it has H*W
+    columns (sl_system.py:605), otherwise rays come from ``cam_K``."""
+    planes = np.asarray(calib["wPlaneCol"])
+    if planes.shape[0] == 4:
+        planes = planes.T
+    if planes.ndim != 2 or planes.shape[1] < 4:
+        raise ValueError(f"wPlaneCol has shape {planes.shape}; expected (Wp, 4) or (4, Wp)")
+    Nc = calib.get("Nc")
+    Nc = None if Nc is None else np.asarray(Nc)
+    if Nc is not None and not (Nc.ndim == 2 and Nc.shape[0] == 3 and Nc.shape[1] == H * W):
+        Nc = None
+    Oc = _f64c(calib["Oc"]).reshape(-1)
+    if Oc.size != 3:
+        raise ValueError("Oc must have 3 entries")
+    return _f64c(calib["cam_K"]).reshape(3, 3), Oc, _f64c(planes[:, :4]), None if Nc is None else _f64c(Nc)
+
+
+class Reconstructor:
+    """Owns one device context.  Thread-safe: calls are serialised per context."""
+
+    def __init__(self, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("structured-light GPU path: no HIP device visible (the product path has no "
+                               "CPU fallback)")
+        dev = torch.device(device if device is not None else "cuda")
+        if dev.type != "cuda":
+            raise ValueError(f"Reconstructor needs a cuda device, got {dev}")
+        self.device = torch.device("cuda", dev.index if dev.index is not None else torch.cuda.current_device())
+        self._L = _lib.load()
+        self._ctx = ctypes.c_void_p()
+        _lib.check(self._L.sl_ctx_create(self.device.index, ctypes.byref(self._ctx)), None, "sl_ctx_create")
+        self._lock = threading.RLock()
+        self._calib_key = None
+        self._H = self._W = None
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            self._L.sl_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+    # ------------------------------------------------------------ calibration
+    def set_calibration(self, calib: dict, H: int, W: int) -> None:
+        K, Oc, planes, Nc = calibration_arrays(calib, H, W)
+        h = hashlib.blake2b(digest_size=16)
+        for a in (K, Oc, planes):
+            h.update(a.tobytes())
+        if Nc is not None:
+            h.update(Nc[:, :: max(1, Nc.shape[1] // 4096)].tobytes())
+            h.update(str(id(calib.get("Nc"))).encode())
+        key = (H, W, h.hexdigest(), Nc is None)
+        with self._lock:
+            if key == self._calib_key:
+                return
+            _lib.check(self._L.sl_set_calib(self._ctx, H, W, K.ctypes.data, Oc.ctypes.data, planes.ctypes.data,
+                                            planes.shape[0], None if Nc is None else Nc.ctypes.data),
+                       self._ctx, "sl_set_calib")
+            self._calib_key = key
+            self._H, self._W = H, W
+
+    def reserve(self, max_views: int, max_px: int) -> None:
+        with self._lock:
+            _lib.check(self._L.sl_ctx_reserve(self._ctx, max_views, max_px), self._ctx, "sl_ctx_reserve")
+
+    # --------------------------------------------------------------- compute
+    def _stream(self, stream):
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return s.cuda_stream
+
+    def decode_triangulate(self, stack: torch.Tensor, n_cols: int = 1920, n_rows: int = 1080, *,
+                           texture: torch.Tensor | None = None, mask_mode: str = "adaptive",
+                           maps: bool = False, cloud: bool = True, xyz_dtype=torch.float32,
+                           poses: torch.Tensor | None = None, stream=None, out: dict | None = None):
+        """Fused decode (+ triangulation) of a device stack.
+
+        ``stack`` uint8 [n_img, H, W] or [V, n_img, H, W] on this device;
+        ``texture`` uint8 BGR [H, W, 3] / [V, H, W, 3] or None (white plane
+        replicated).  Returns a dict with ``col_map``/``row_map`` int32,
+        ``mask`` bool ([V,H,W], when ``maps``) and ``cloud`` (a ``Cloud``,
+        when ``cloud``).  Asynchronous on ``stream``; ``out`` reuses buffers.
+        """
+        if stack.dtype != torch.uint8 or stack.device != self.device:
+            raise ValueError("stack must be a uint8 tensor on the reconstructor's device")
+        if stack.dim() == 3:
+            stack = stack.unsqueeze(0)
+            texture = None if texture is None else texture.unsqueeze(0)
+            poses = None if poses is None else poses.reshape(1, 4, 4)
+        if stack.dim() != 4:
+            raise ValueError("stack must be [n_img, H, W] or [V, n_img, H, W]")
+        if stack.stride(3) != 1 or stack.stride(2) != stack.shape[3] or stack.stride(1) != stack.shape[2] * stack.shape[3]:
+            stack = stack.contiguous()
+        V, n_img, H, W = stack.shape
+        if texture is not None:
+            if texture.shape != (V, H, W, 3) or texture.dtype != torch.uint8:
+                raise ValueError(f"texture must be uint8 [{V},{H},{W},3]")
+            texture = texture.contiguous()
+        if poses is not None:
+            poses = poses.to(device=self.device, dtype=torch.float64).reshape(V, 16).contiguous()
+        if mask_mode not in MASK_MODES:
+            raise ValueError(f"mask_mode must be one of {sorted(MASK_MODES)}")
+        if not maps and not cloud:
+            raise ValueError("nothing to compute")
+        out = {} if out is None else out
+        col = row = msk = xyz = bgr = vo = None
+        if maps:
+            col = out.get("col_map")
+            if col is None or col.shape != (V, H, W):
+                col = out["col_map"] = torch.empty((V, H, W), dtype=torch.int32, device=self.device)
+                out["row_map"] = torch.empty((V, H, W), dtype=torch.int32, device=self.device)
+                out["mask_u8"] = torch.empty((V, H, W), dtype=torch.uint8, device=self.device)
+            row, msk = out["row_map"], out["mask_u8"]
+        cap = V * H * W
+        xyz_code = _lib.SL_XYZ_F64 if xyz_dtype == torch.float64 else _lib.SL_XYZ_F32
+        if cloud:
+            xyz = out.get("xyz")
+            if xyz is None or xyz.shape[0] < cap or xyz.dtype != xyz_dtype:
+                xyz = out["xyz"] = torch.empty((cap, 3), dtype=xyz_dtype, device=self.device)
+                out["bgr"] = torch.empty((cap, 3), dtype=torch.uint8, device=self.device)
+                out["view_offsets"] = torch.empty(V + 1, dtype=torch.int64, device=self.device)
+            bgr, vo = out["bgr"], out["view_offsets"]
+            if vo.shape[0] != V + 1:
+                vo = out["view_offsets"] = torch.empty(V + 1, dtype=torch.int64, device=self.device)
+        with self._lock:
+            if cloud and (self._H, self._W) != (H, W):
+                raise ValueError(f"calibration is for {self._W}x{self._H}, stack is {W}x{H}")
+            _lib.check(self._L.sl_decode_triangulate(
+                self._ctx, stack.data_ptr(), stack.stride(0), V, n_img, H, W, int(n_cols), int(n_rows),
+                _ptr(texture), 3 * H * W if texture is None else texture.stride(0), MASK_MODES[mask_mode],
+                _ptr(poses), _ptr(col), _ptr(row), _ptr(msk), _ptr(xyz), xyz_code, _ptr(bgr),
+                cap if cloud else 0, _ptr(vo), self._stream(stream)), self._ctx, "sl_decode_triangulate")
+        res = {}
+        if maps:
+            res["col_map"], res["row_map"], res["mask"] = col, row, msk.view(torch.bool)
+        if cloud:
+            res["cloud"] = Cloud(xyz, bgr, vo)
+        return res
+
+    def triangulate_maps(self, col_map: torch.Tensor, mask: torch.Tensor, texture: torch.Tensor, *,
+                         xyz_dtype=torch.float64, poses=None, stream=None) -> Cloud:
+        """reconstruct_point_cloud on device maps: col_map int32 [V,H,W] (or
+        [H,W]), mask bool/uint8, texture uint8 BGR [V,H,W,3]."""
+        if col_map.dim() == 2:
+            col_map, mask, texture = col_map[None], mask[None], texture[None]
+            poses = None if poses is None else poses.reshape(1, 4, 4)
+        V, H, W = col_map.shape
+        col_map = col_map.to(device=self.device, dtype=torch.int32).contiguous()
+        mask = mask.to(device=self.device).to(torch.uint8).contiguous()
+        texture = texture.to(device=self.device, dtype=torch.uint8).contiguous()
+        if mask.shape != (V, H, W) or texture.shape != (V, H, W, 3):
+            raise ValueError("mask / texture shapes do not match col_map")
+        if poses is not None:
+            poses = poses.to(device=self.device, dtype=torch.float64).reshape(V, 16).contiguous()
+        cap = V * H * W
+        xyz = torch.empty((cap, 3), dtype=xyz_dtype, device=self.device)
+        bgr = torch.empty((cap, 3), dtype=torch.uint8, device=self.device)
+        vo = torch.empty(V + 1, dtype=torch.int64, device=self.device)
+        xyz_code = _lib.SL_XYZ_F64 if xyz_dtype == torch.float64 else _lib.SL_XYZ_F32
+        with self._lock:
+            if (self._H, self._W) != (H, W):
+                raise ValueError(f"calibration is for {self._W}x{self._H}, maps are {W}x{H}")
+            _lib.check(self._L.sl_triangulate_maps(
+                self._ctx, col_map.data_ptr(), mask.data_ptr(), texture.data_ptr(), V, H, W, _ptr(poses),
+                xyz.data_ptr(), xyz_code, bgr.data_ptr(), cap, vo.data_ptr(), self._stream(stream)),
+                self._ctx, "sl_triangulate_maps")
+        return Cloud(xyz, bgr, vo)
+
+    def sync(self, stream=None) -> None:
+        """Wait for this context's work and raise on device-side failures."""
+        with self._lock:
+            _lib.check(self._L.sl_sync(self._ctx, self._stream(stream)), self._ctx, "sl_sync")
+
+    def profile_enable(self, max_launches: int) -> None:
+        """Record HIP events around k_stats / k_decode of the next launches."""
+        with self._lock:
+            _lib.check(self._L.sl_profile_enable(self._ctx, int(max_launches)), self._ctx, "sl_profile_enable")
+
+    def profile_read(self):
+        """-> (k_stats ms total, k_decode ms total, launches) since last read."""
+        a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        with self._lock:
+            _lib.check(self._L.sl_profile_read(self._ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)),
+                       self._ctx, "sl_profile_read")
+        return a.value, b.value, n.value
+
+    def last_thresholds(self, view: int = 0):
+        nf, dr = ctypes.c_float(), ctypes.c_float()
+        tw, tc = ctypes.c_int(), ctypes.c_int()
+        with self._lock:
+            _lib.check(self._L.sl_last_thresholds(self._ctx, view, ctypes.byref(nf), ctypes.byref(dr),
+                                                  ctypes.byref(tw), ctypes.byref(tc)), self._ctx,
+                       "sl_last_thresholds")
+        return np.float32(nf.value), np.float32(dr.value), tw.value, tc.value
+
+
+_engines: dict = {}
+_engines_lock = threading.Lock()
+
+
+def engine(device=None) -> Reconstructor:
+    """Process-wide Reconstructor for ``device`` (default: current GPU)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("structured-light GPU path: no HIP device visible (no CPU fallback)")
+    idx = torch.device(device).index if device is not None else torch.cuda.current_device()
+    idx = torch.cuda.current_device() if idx is None else idx
+    with _engines_lock:
+        if idx not in _engines:
+            _engines[idx] = Reconstructor(torch.device("cuda", idx))
+        return _engines[idx]

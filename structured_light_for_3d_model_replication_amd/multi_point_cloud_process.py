@@ -1,0 +1,100 @@
+"""Drop-in for the processing functions of ``multi_point_cloud_process.py``
+(the batch GUI) and ``Old/process_cloud.py`` (the CLI).
+
+Same names and signatures as multi_point_cloud_process.py:13-131:
+``load_calibration``, ``gray_decode`` (FIXED mask: white > 40 and
+white - black > 10, :36-38), ``reconstruct_point_cloud``, ``save_ply``; plus
+``process_single`` / ``process_batch``, the per-folder loop of the GUI's
+worker thread (:201-257) without Tk.  ``process_batch`` decodes the subfolders
+as one multi-view GPU batch when they share a frame size.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import scipy.io
+import torch
+
+from . import core, io, ply
+from .sl_system import reconstruct_point_cloud  # identical arithmetic (:73-119)
+
+__all__ = ["load_calibration", "gray_decode", "reconstruct_point_cloud", "save_ply", "process_single",
+           "process_batch"]
+
+
+def load_calibration(calib_path):
+    """multi_point_cloud_process.py:13-21 (Old/process_cloud.py:8-23 adds the
+    FileNotFoundError, kept here)."""
+    if not os.path.exists(calib_path):
+        raise FileNotFoundError(f"Calibration file not found at {calib_path}")
+    data = scipy.io.loadmat(calib_path)
+    return {"Nc": data["Nc"], "Oc": data["Oc"], "wPlaneCol": data["wPlaneCol"], "wPlaneRow": data["wPlaneRow"],
+            "cam_K": data["cam_K"]}
+
+
+def gray_decode(folder, n_cols=1920, n_rows=1080, *, device=None):
+    """multi_point_cloud_process.py:23-71 (fixed-threshold mask)."""
+    stack, texture, _ = io.read_stack(folder)
+    eng = core.engine(device)
+    res = eng.decode_triangulate(torch.from_numpy(stack).to(eng.device), n_cols, n_rows, mask_mode="fixed",
+                                 maps=True, cloud=False)
+    eng.sync()
+    return (res["col_map"][0].cpu().numpy(), res["row_map"][0].cpu().numpy(), res["mask"][0].cpu().numpy(),
+            texture)
+
+
+save_ply = ply.save_ply
+
+
+def process_single(scan_dir, calib_data, *, device=None, log=print):
+    """multi_point_cloud_process.py:201-213: decode, reconstruct, save."""
+    out_path = os.path.join(scan_dir, os.path.basename(scan_dir) + ".ply")
+    log(f"-> Decoding images in {os.path.basename(scan_dir)}...")
+    c_map, r_map, mask, texture = gray_decode(scan_dir, device=device)
+    log("-> Reconstructing 3D points...")
+    points, colors = reconstruct_point_cloud(c_map, r_map, mask, texture, calib_data, device=device)
+    log(f"-> Saving {len(points)} points...")
+    save_ply(points, colors, out_path)
+    return out_path
+
+
+def process_batch(parent_dir, calib_data, *, n_cols=1920, n_rows=1080, device=None, write=True, log=print):
+    """Batch mode of multi_point_cloud_process.py:241-257: every subfolder with
+    images is one view.  Views of equal size are decoded + triangulated in ONE
+    fused GPU launch (merged cloud, per-view offsets); per-view PLY files are
+    written exactly as the reference writes them.  Returns {folder: (P, C)}."""
+    subfolders = sorted(f.path for f in os.scandir(parent_dir) if f.is_dir())
+    views = [f for f in subfolders if io.list_stack_files(f)]
+    for f in subfolders:
+        if f not in views:
+            log(f"Skipping {os.path.basename(f)} (No images found).")
+    if not views:
+        return {}
+    stacks, texes = [], []
+    for f in views:
+        st, tex, _ = io.read_stack(f)
+        stacks.append(st)
+        texes.append(tex)
+    shapes = {s.shape for s in stacks}
+    if len(shapes) != 1:
+        raise ValueError(f"batch views differ in stack shape: {sorted(shapes)}")
+    eng = core.engine(device)
+    H, W = stacks[0].shape[1:]
+    eng.set_calibration(calib_data, H, W)
+    res = eng.decode_triangulate(torch.from_numpy(np.stack(stacks)).to(eng.device), n_cols, n_rows,
+                                 texture=torch.from_numpy(np.stack(texes)).to(eng.device), mask_mode="fixed",
+                                 maps=False, cloud=True, xyz_dtype=torch.float64)
+    eng.sync()
+    cloud = res["cloud"]
+    off = cloud.offsets()
+    xyz = cloud.xyz[: off[-1]].cpu().numpy()
+    bgr = cloud.bgr[: off[-1]].cpu().numpy()
+    out = {}
+    for v, f in enumerate(views):
+        P, C = xyz[off[v]:off[v + 1]], bgr[off[v]:off[v + 1]]
+        out[f] = (P, C)
+        if write:
+            save_ply(P, C, os.path.join(f, os.path.basename(f) + ".ply"))
+            log(f"Saved: {os.path.basename(f)}.ply ({len(P)} points)")
+    return out
