@@ -1,0 +1,62 @@
+"""Kernel-level timing of k_stats / k_decode variants (HIP events), one process.
+
+    python scripts/kbench.py [--config c2] [--reps 20]
+Prints one line per variant: mode, k_stats us, k_decode us, algorithmic GB/s.
+Set SLGPU_DEBUG (1 = tile from blockIdx, 2 = no look-back) for ablations.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from structured_light_for_3d_model_replication_amd import core, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--H", type=int, default=2160)
+ap.add_argument("--W", type=int, default=3840)
+ap.add_argument("--views", type=int, default=1)
+ap.add_argument("--reps", type=int, default=20)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+rig = synth.Rig(H=a.H, W=a.W)
+cal = synth.make_calibration(rig, with_Nc=False)
+sts, txs = zip(*[synth.render_stack(rig, seed=7 + v, device=dev) for v in range(a.views)])
+st = torch.stack(sts)
+tx = torch.stack(txs)
+eng = core.Reconstructor(dev)
+eng.set_calibration(cal, a.H, a.W)
+px = a.views * a.H * a.W
+# HBM copy roof for reference: 2 x bytes moved
+buf = st.clone()
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+for _ in range(3):
+    buf.copy_(st)
+e0.record()
+for _ in range(a.reps):
+    buf.copy_(st)
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / a.reps
+print(json.dumps({"variant": "torch_copy", "us": ms * 1e3, "GBps": 2 * st.numel() / ms / 1e6}))
+for name, kw in [("maps+cloud", dict(maps=True, cloud=True)), ("cloud", dict(maps=False, cloud=True)),
+                 ("maps", dict(maps=True, cloud=False)),
+                 ("maps+cloud fixed", dict(maps=True, cloud=True, mask_mode="fixed"))]:
+    out = {}
+    for _ in range(3):
+        eng.decode_triangulate(st, texture=tx, out=out, **kw)
+    eng.sync()
+    eng.profile_enable(a.reps)
+    for _ in range(a.reps):
+        eng.decode_triangulate(st, texture=tx, out=out, **kw)
+    s_ms, d_ms, n = eng.profile_read()
+    eng.sync()
+    npts = int(out["view_offsets"][-1].item()) if "view_offsets" in out else 0
+    planes = st.shape[1] if kw.get("maps") else 2 + 2 * 11
+    b = px * planes + (3 * px + 15 * npts if kw.get("cloud") else 0) + (9 * px if kw.get("maps") else 0)
+    print(json.dumps({"variant": name, "dbg": os.environ.get("SLGPU_DEBUG", "0"), "stats_us": 1e3 * s_ms / n,
+                      "decode_us": 1e3 * d_ms / n, "alg_GBps": b / (d_ms / n) / 1e6, "points": npts}))

@@ -27,6 +27,7 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -60,15 +61,17 @@ constexpr unsigned long long kFlagPre = 2ull << 62;
 constexpr unsigned long long kValMask = (1ull << 62) - 1;
 constexpr unsigned kSpinLimit = 1u << 22;
 
+constexpr int kStatBlocks = 256;  // k_stats blocks per view (max)
+constexpr int kReps = 16;         // histogram replicas per view
+constexpr int kSlot = 272;        // u32 per replica: 256 bins + max + pad (1088 B)
+
 struct ViewStats {
-  unsigned hist[256];   // histogram of the black plane
-  unsigned max_c;       // max(white - black) + 256 (0 = nothing seen)
   unsigned done;        // k_stats blocks finished for this view
   int thr_white;        // mask: white > thr_white
   int thr_contrast;     //       white - black > thr_contrast
   float noise_floor;    // np.percentile(black, 95) (float32)
   float dynamic_range;  // max(white - black) (float32)
-  unsigned pad[26];
+  unsigned pad[11];
 };
 static_assert(sizeof(ViewStats) % 64 == 0, "ViewStats keeps 64-B alignment");
 
@@ -91,6 +94,7 @@ struct Params {
   int nc, nr, kc, kr;  // code bits and available bit planes (pairs)
   int mask_mode;
   int mode;
+  int dbg;  // measurement-only ablations (SLGPU_DEBUG): 1 = tile from blockIdx, 2 = no look-back
   int Wp;
   const double4* planes;
   const double* xn;
@@ -105,6 +109,7 @@ struct Params {
   uint8_t* bgr;
   int64_t* view_offsets;
   ViewStats* stats;
+  unsigned* part;  // k_stats histogram replicas [view][kReps][kSlot]
   unsigned long long* status;
   Header* hdr;
 };
@@ -166,9 +171,16 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 }
 
 // --------------------------------------------------------------- k_stats ----
-// grid (bx, n_views).  Clears k_decode's look-back words and ticket; with the
-// adaptive mask also builds the per-view histogram/max and, in the last block
-// of each view, the float32 thresholds (numpy 2.x percentile, method 'linear').
+// grid (bx <= kStatBlocks, n_views).  Clears k_decode's look-back words and
+// ticket; with the adaptive mask also builds, per view, the 256-bin histogram
+// of the black plane and max(white - black):
+//   * per-wave LDS histograms, then no-return device atomics into one of
+//     kReps replicas of the view's histogram (blockIdx % kReps), so no more
+//     than bx/kReps blocks ever add to one address;
+//   * every wave drains its atomics (vmcnt(0)), then one lane adds to the
+//     view's arrival counter; the block whose add is last reads (and zeroes)
+//     the replicas with returning atomics and evaluates numpy's float32
+//     percentile recipe.  The replicas are left zeroed for the next call.
 __global__ __launch_bounds__(kThreads) void k_stats(Params p, int64_t n_status, int do_stats,
                                                     int vec) {
   const int tid = threadIdx.x;
@@ -181,6 +193,7 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p, int64_t n_status, 
 
   __shared__ unsigned sh[kWaves][256];
   __shared__ unsigned cdf[256];
+  __shared__ int s_max[kWaves];
   __shared__ long long s_k[2];
   __shared__ int s_v[2];
   __shared__ float s_gamma;
@@ -207,26 +220,53 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p, int64_t n_status, 
       }
     }
   }
-  __syncthreads();
-  {
-    const unsigned s = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
-    if (s) atomicAdd(&p.stats[view].hist[tid], s);
-  }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
-  if ((tid & 63) == 0 && mx > -1024) atomicMax(&p.stats[view].max_c, static_cast<unsigned>(mx + 256));
-  __threadfence();
+  if ((tid & 63) == 0) s_max[wid] = mx;
   __syncthreads();
-  if (tid == 0) s_last = (atomicAdd(&p.stats[view].done, 1u) == gridDim.x - 1);
+  unsigned* rep = p.part + (static_cast<int64_t>(view) * kReps + blockIdx.x % kReps) * kSlot;
+  {
+    const unsigned cnt = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
+    if (cnt) atomicAdd(rep + tid, cnt);
+  }
+  if (tid == 0) {
+    int m = s_max[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) m = max(m, s_max[w]);
+    if (m > -1024) atomicMax(rep + 256, static_cast<unsigned>(m + 1024));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(&p.stats[view].done, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == gridDim.x - 1);
+  }
   __syncthreads();
   if (!s_last) return;
 
-  // ---- last block of this view: thresholds (and reset the accumulators) ----
-  __threadfence();
-  const unsigned h = atomicExch(&p.stats[view].hist[tid], 0u);
+  // ---- last block of this view: read + zero the replicas, thresholds ----
+  unsigned* reps = p.part + static_cast<int64_t>(view) * kReps * kSlot;
+  unsigned h = 0u;
+  {
+    unsigned v[kReps];
+#pragma unroll
+    for (int r = 0; r < kReps; ++r) v[r] = atomicExch(reps + r * kSlot + tid, 0u);
+#pragma unroll
+    for (int r = 0; r < kReps; ++r) h += v[r];
+  }
+  int m = -1024;
+  if (tid < kReps) {
+    const unsigned mv = atomicExch(reps + tid * kSlot + 256, 0u);
+    if (mv) m = static_cast<int>(mv) - 1024;
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
   cdf[tid] = h;
+  if ((tid & 63) == 0) s_max[wid] = m;
+  if (tid == 0) __hip_atomic_store(&p.stats[view].done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {  // inclusive scan
+  for (int d = 1; d < 256; d <<= 1) {  // inclusive scan -> cdf
     const unsigned t = tid >= d ? cdf[tid - d] : 0u;
     __syncthreads();
     cdf[tid] += t;
@@ -235,7 +275,8 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p, int64_t n_status, 
   if (tid == 0) {
     // np.percentile(black_f32, 95): q = f32(95)/f32(100); virtual index
     // (n-1)*q in float32; neighbours floor / floor+1, both clamped to n-1 when
-    // the index is >= n-1 (numpy/lib/_function_base_impl.py _get_indexes).
+    // the index is >= n-1 (numpy/lib/_function_base_impl.py _get_indexes);
+    // gamma = index - floor (exact in float32).
     const long long n = p.HW;
     const float q = 95.0f / 100.0f;
     const float fn1 = static_cast<float>(n - 1);
@@ -271,16 +312,17 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p, int64_t n_status, 
     const float diff = b - a;
     float nf = a + diff * gamma;
     if (gamma >= 0.5f) nf = b - diff * (1.0f - gamma);
-    const unsigned mc = atomicExch(&p.stats[view].max_c, 0u);
-    const float dr = static_cast<float>(static_cast<int>(mc) - 256);
-    // white, contrast are integers: x > t  <=>  x > floor(t)
+    int mc = s_max[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) mc = max(mc, s_max[w]);
+    const float dr = static_cast<float>(mc);
+    // white and contrast are integers: x > t  <=>  x > floor(t)
     const float tw = nf * 1.5f;
     const float tc = dr * 0.05f;
     p.stats[view].noise_floor = nf;
     p.stats[view].dynamic_range = dr;
     p.stats[view].thr_white = static_cast<int>(floorf(tw));
     p.stats[view].thr_contrast = static_cast<int>(floorf(tc));
-    atomicExch(&p.stats[view].done, 0u);
   }
 }
 
@@ -303,7 +345,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_decode(Params p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(&p.hdr->ticket, 1u);
+  if (tid == 0) s_tile = (p.dbg & 1) ? blockIdx.x : atomicAdd(&p.hdr->ticket, 1u);
   __syncthreads();
   const unsigned tile = s_tile;
   const int view = static_cast<int>(tile / p.tiles_per_view);
@@ -591,8 +633,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_decode(Params p) {
   if (wid == 0) {
     unsigned long long* st = p.status;
     if (lane == 0) st_status(st + tile, (tile == 0 ? kFlagPre : kFlagAgg) | static_cast<unsigned long long>(total));
-    long long excl = 0;
-    if (tile > 0) {
+    long long excl = (p.dbg & 2) ? static_cast<long long>(tile) * kTile : 0;
+    if (tile > 0 && !(p.dbg & 2)) {
       long long j = static_cast<long long>(tile) - 1;
       unsigned spins = 0;
       for (;;) {
@@ -709,9 +751,12 @@ struct sl_ctx {
   Header* d_hdr = nullptr;
   ViewStats* d_stats = nullptr;
   int64_t cap_views = 0;
+  unsigned* d_part = nullptr;
+  int64_t cap_part = 0;
   unsigned long long* d_status = nullptr;
   int64_t cap_status = 0;
   int last_views = 0;
+  int dbg = 0;
   // optional per-launch HIP-event timing of k_stats / k_decode
   std::vector<hipEvent_t> prof_ev;  // 3 events per launch slot
   int prof_n = 0;
@@ -752,6 +797,8 @@ int grow(sl_ctx* c, T** ptr, int64_t* cap, int64_t need) {
 int ensure_scratch(sl_ctx* c, int64_t views, int64_t tiles) {
   int r = grow(c, &c->d_stats, &c->cap_views, views);
   if (r) return r;
+  r = grow(c, &c->d_part, &c->cap_part, views * kReps * kSlot);
+  if (r) return r;
   return grow(c, &c->d_status, &c->cap_status, tiles);
 }
 
@@ -785,13 +832,16 @@ int launch(sl_ctx* c, Params& p, bool vec, bool do_stats, hipStream_t s) {
   int r = ensure_scratch(c, p.n_views, tiles);
   if (r) return r;
   p.stats = c->d_stats;
+  p.part = c->d_part;
   p.status = c->d_status;
   p.hdr = c->d_hdr;
   c->last_views = p.n_views;
   // k_stats: enough blocks to cover the views with ~2K workgroups in total
   int bx = 1;
   if (do_stats) {
-    bx = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(p.tiles_per_view, 2048 / std::max(1, p.n_views))));
+    bx = static_cast<int>(std::max<int64_t>(
+        1, std::min<int64_t>({static_cast<int64_t>(p.tiles_per_view), int64_t{kStatBlocks},
+                              std::max<int64_t>(1, 2048 / p.n_views)})));
   } else {
     bx = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, (tiles + 255) / 256)));
   }
@@ -824,6 +874,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
   *out = nullptr;
   sl_ctx* c = new sl_ctx();
   c->device = device;
+  if (const char* d = getenv("SLGPU_DEBUG")) c->dbg = atoi(d);
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_hdr), sizeof(Header));
   if (e == hipSuccess) e = hipMemset(c->d_hdr, 0, sizeof(Header));
@@ -841,6 +892,7 @@ void sl_ctx_destroy(sl_ctx* c) {
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (void* ptr : {static_cast<void*>(c->d_planes), static_cast<void*>(c->d_xn), static_cast<void*>(c->d_yn),
                     static_cast<void*>(c->d_nc), static_cast<void*>(c->d_hdr), static_cast<void*>(c->d_stats),
+                    static_cast<void*>(c->d_part),
                     static_cast<void*>(c->d_status)})
     if (ptr) (void)hipFree(ptr);
   delete c;
@@ -929,6 +981,7 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.o0 = c->Oc[0];
   p.o1 = c->Oc[1];
   p.o2 = c->Oc[2];
+  p.dbg = c->dbg;
 }
 
 int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int n_views, int n_img,
