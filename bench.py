@@ -4,15 +4,16 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-A step is one pass of the fused hot path over one batch of synthetic views
-resident in HBM: k_stats (histogram/threshold pre-pass) + k_decode (Gray decode,
-mask, Gray->binary, ray/plane triangulation, ordered compaction), producing
-what the reference's gray_decode + reconstruct_point_cloud return: col_map,
-row_map, mask and the (xyz, BGR) cloud.  Default workload = BASELINE config 2:
-one 3840x2160 view, 11+11-bit column+row Gray code with inverses (46 planes),
-per GPU per step.  Multi-GPU: weak scaling, views sharded over ranks with no
-data-path collective; the RCCL gather of the clouds to rank 0 is timed
-separately ("gather_ms").
+A step is one pass of the hot path over one batch of synthetic views resident
+in HBM -- k_stats (adaptive-mask thresholds), k_decode (Gray decode, mask,
+Gray->binary, point/no-point decision), k_scan (tile offsets), k_cloud (f64
+ray/plane intersection, ordered stores) -- producing what the reference's
+gray_decode + reconstruct_point_cloud return: col_map, row_map, mask and the
+(xyz, BGR) cloud.  Default workload = BASELINE config 2: one 3840x2160 view,
+11+11-bit column+row Gray code with inverses (46 planes), per GPU per step.
+Multi-GPU: weak scaling, views sharded over ranks with no data-path
+collective; the RCCL gather of the clouds to rank 0 is timed separately
+("gather_ms").
 """
 from __future__ import annotations
 
@@ -57,14 +58,20 @@ def parse():
     return ap.parse_args()
 
 
-def algorithmic_bytes(H, W, n_planes, n_points, maps=True):
-    """H*W*(2+2(nc+nr)) stack + 3*H*W texture + 15*N_out,
-    + 8*H*W col/row int32 + H*W mask bytes when the maps are written."""
+def path_bytes(H, W, n_planes, n_points, maps=True):
+    """SURVEY.md §8(d), whole path: H*W*(2+2(nc+nr)) stack + 3*H*W texture
+    + 15*N_out, + 8*H*W col/row int32 + H*W mask bytes when maps are written."""
     px = H * W
     b = n_planes * px + 3 * px + 15 * n_points
     if maps:
         b += 9 * px
     return b
+
+
+def decode_bytes(H, W, n_planes, maps=True):
+    """Algorithmic bytes of k_decode alone: the stack it streams + the maps it
+    writes (its 2-byte per-pixel records for k_cloud are overhead, not counted)."""
+    return H * W * (n_planes + (9 if maps else 0))
 
 
 def cpu_baseline(stack_h, tex_h, calib, budget_s):
@@ -133,7 +140,7 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    stats_ms, decode_ms, nl = eng.profile_read()
+    stats_ms, decode_ms, cloud_ms, nl = eng.profile_read()
     eng.sync()
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if world > 1:
@@ -167,8 +174,9 @@ def main():
         px_step = V * H * W
         value = world * px_step * a.steps / el
         dec_avg_ms = decode_ms / max(nl, 1)
-        ab = algorithmic_bytes(H, W, n_planes, n_pts / V, maps=True) * V
+        ab = decode_bytes(H, W, n_planes, maps=True) * V
         achieved = ab / (dec_avg_ms * 1e-3) / 1e9
+        path_b = path_bytes(H, W, n_planes, n_pts / V, maps=True) * V
         traffic = None
         if os.path.exists(a.traffic):
             try:
@@ -206,9 +214,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_decode", "kernel_avg_ms": dec_avg_ms,
-                         "algorithmic_bytes_per_launch": ab},
+                         "algorithmic_bytes_per_launch": ab,
+                         "bytes_note": "stack planes read + col/row/mask maps written, per launch"},
+            "path": {"algorithmic_bytes_per_step": path_b,
+                     "GBps": path_b / (el / a.steps) / 1e9,
+                     "kernel_avg_ms": {"k_stats": stats_ms / max(nl, 1), "k_decode": dec_avg_ms,
+                                       "k_scan+k_cloud": cloud_ms / max(nl, 1)}},
             "cpu_baseline": cpu,
-            "k_stats_avg_ms": stats_ms / max(nl, 1),
             "points_per_view": n_pts / V,
             "cloud_only_px_per_s": world * px_step * a.steps / el_cloud,
             "gather_ms": gather_ms,

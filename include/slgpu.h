@@ -133,13 +133,15 @@ int sl_sync(sl_ctx* ctx, void* stream);
 int sl_last_thresholds(sl_ctx* ctx, int view, float* noise_floor, float* dynamic_range,
                        int* thr_white, int* thr_contrast);
 
-/* Timing: with max_launches > 0, each later launch (up to that many) records
- * HIP events on its stream around k_stats and around k_decode.  0 disables. */
+/* Timing: with max_launches > 0, each later call (up to that many) records HIP
+ * events on its stream around its kernels k_stats, k_decode and k_cloud.
+ * 0 disables. */
 int sl_profile_enable(sl_ctx* ctx, int max_launches);
 
-/* Blocking: summed event time (ms) of k_stats and k_decode over the recorded
- * launches since the last read, and their count; then restarts recording. */
-int sl_profile_read(sl_ctx* ctx, double* stats_ms, double* decode_ms, int* launches);
+/* Blocking: summed event time (ms) of k_stats, k_decode and k_cloud over the
+ * recorded calls since the last read, and their count; restarts recording. */
+int sl_profile_read(sl_ctx* ctx, double* stats_ms, double* decode_ms, double* cloud_ms,
+                    int* launches);
 
 #ifdef __cplusplus
 }

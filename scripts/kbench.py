@@ -53,10 +53,12 @@ for name, kw in [("maps+cloud", dict(maps=True, cloud=True)), ("cloud", dict(map
     eng.profile_enable(a.reps)
     for _ in range(a.reps):
         eng.decode_triangulate(st, texture=tx, out=out, **kw)
-    s_ms, d_ms, n = eng.profile_read()
+    s_ms, d_ms, c_ms, n = eng.profile_read()
     eng.sync()
     npts = int(out["view_offsets"][-1].item()) if "view_offsets" in out else 0
     planes = st.shape[1] if kw.get("maps") else 2 + 2 * 11
     b = px * planes + (3 * px + 15 * npts if kw.get("cloud") else 0) + (9 * px if kw.get("maps") else 0)
+    tot = (s_ms + d_ms + c_ms) / n
     print(json.dumps({"variant": name, "dbg": os.environ.get("SLGPU_DEBUG", "0"), "stats_us": 1e3 * s_ms / n,
-                      "decode_us": 1e3 * d_ms / n, "alg_GBps": b / (d_ms / n) / 1e6, "points": npts}))
+                      "decode_us": 1e3 * d_ms / n, "cloud_us": 1e3 * c_ms / n, "total_us": 1e3 * tot,
+                      "alg_GBps_total": b / tot / 1e6, "points": npts}))

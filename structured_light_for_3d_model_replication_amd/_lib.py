@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libslgpu.so")
+# SLGPU_LIB selects an alternative build (measurement of build variants only)
+LIB_PATH = os.environ.get("SLGPU_LIB") or os.path.join(_HERE, "libslgpu.so")
 
 SL_OK = 0
 SL_EINVAL = -1
@@ -50,7 +51,7 @@ _SIGS = {
                                   ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
     "sl_profile_enable": (_i32, [_vp, _i32]),
     "sl_profile_read": (_i32, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
-                                ctypes.POINTER(_i32)]),
+                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]),
 }
 
 _lock = threading.Lock()

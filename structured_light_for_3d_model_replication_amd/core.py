@@ -240,12 +240,12 @@ class Reconstructor:
             _lib.check(self._L.sl_profile_enable(self._ctx, int(max_launches)), self._ctx, "sl_profile_enable")
 
     def profile_read(self):
-        """-> (k_stats ms total, k_decode ms total, launches) since last read."""
-        a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        """-> (k_stats ms, k_decode ms, k_cloud ms, calls) summed since last read."""
+        a, b, c, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
         with self._lock:
-            _lib.check(self._L.sl_profile_read(self._ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)),
-                       self._ctx, "sl_profile_read")
-        return a.value, b.value, n.value
+            _lib.check(self._L.sl_profile_read(self._ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+                                               ctypes.byref(n)), self._ctx, "sl_profile_read")
+        return a.value, b.value, c.value, n.value
 
     def last_thresholds(self, view: int = 0):
         nf, dr = ctypes.c_float(), ctypes.c_float()

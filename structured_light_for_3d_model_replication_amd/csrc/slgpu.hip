@@ -9,18 +9,19 @@
 //                  |n.r| > 1e-6, t = -(n.Oc + d)/(n.r), P = Oc + r t, BGR colour)
 //
 // Kernels (one HIP stream, no host synchronisation between them):
-//   k_stats   : 256-bin histogram of the black plane + max(white - black) per view,
-//               merged with device atomics; the last block of each view turns them
-//               into the float32 np.percentile(black, 95) recipe and integer
-//               thresholds.  Also clears the look-back state of k_decode.
-//   k_decode  : one 4096-pixel tile per workgroup, 16 pixels per lane.  Streams the
-//               uint8 stack once with 16-byte loads, forms the Gray bits with a
-//               byte-SWAR compare, Gray->binary in registers, masks, intersects the
-//               camera ray with the projector column plane in f64 (reference
-//               operation order, no contraction), and compacts points in pixel
-//               order: workgroup scan + decoupled look-back across tiles taken in
-//               ticket order, staged through LDS so the global stores are 16-byte
-//               coalesced.
+//   k_stats  : (adaptive mask) 256-bin histogram of the black plane + max(white -
+//              black) per view; the last block of each view turns them into the
+//              float32 np.percentile(black, 95) recipe and integer thresholds.
+//   k_decode : one 4096-pixel tile per workgroup.  Streams the uint8 stack once
+//              with 16-byte buffer loads, forms the Gray bits with a byte-SWAR
+//              compare, Gray->binary in registers, applies the mask, writes the
+//              maps, and decides point/no-point per pixel (f32 with an exact
+//              error bound, f64 when undecided); per-pixel 2-byte records and a
+//              point count per tile.
+//   k_scan   : exclusive scan of the tile counts -> tile and view offsets.
+//   k_cloud  : ray/plane intersection in f64 (reference operation order, no
+//              contraction) for the marked pixels, written at tile offset +
+//              wave-ballot rank: the reference's np.where order, coalesced.
 //
 // Everything in this file is compiled with -ffp-contract=off.
 #include <hip/hip_runtime.h>
@@ -45,21 +46,18 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kPx = 16;                  // pixels per lane
 constexpr int kTile = kThreads * kPx;    // pixels per workgroup tile
-constexpr int kRing = 16;                // pattern planes in flight per lane
+#ifndef SLGPU_RING
+#define SLGPU_RING 16
+#endif
+constexpr int kRing = SLGPU_RING;        // pattern planes in flight per lane
 
 // k_decode mode bits
-constexpr int M_MAPS = 1;      // write col/row/mask maps
-constexpr int M_CLOUD = 2;     // triangulate + compact
+constexpr int M_MAPS = 1;      // k_decode: write col/row/mask maps
+constexpr int M_CODES = 2;     // k_decode: point decision, records + tile counts for k_cloud
 constexpr int M_XYZ64 = 4;     // f64 xyz output (else f32)
-constexpr int M_FROMMAPS = 8;  // input is (col_map, mask) instead of the stack
+constexpr int M_FROMMAPS = 8;  // k_decode: input is a caller's (col_map, mask) instead of the stack
 constexpr int M_NC = 16;       // rays from a device Nc table instead of pinhole K
 constexpr int M_ROWS = 32;     // decode the row sequence
-
-// look-back status word: [63:62] flag, [61:0] value
-constexpr unsigned long long kFlagAgg = 1ull << 62;
-constexpr unsigned long long kFlagPre = 2ull << 62;
-constexpr unsigned long long kValMask = (1ull << 62) - 1;
-constexpr unsigned kSpinLimit = 1u << 22;
 
 constexpr int kStatBlocks = 256;  // k_stats blocks per view (max)
 constexpr int kReps = 16;         // histogram replicas per view
@@ -76,14 +74,14 @@ struct ViewStats {
 static_assert(sizeof(ViewStats) % 64 == 0, "ViewStats keeps 64-B alignment");
 
 struct Header {
-  unsigned ticket;  // k_decode tile ticket
-  unsigned error;   // sticky device-side failure (SL_ETIMEOUT)
-  unsigned pad[14];
+  unsigned error;  // sticky device-side failure (reported by sl_sync as SL_ETIMEOUT)
+  unsigned pad[15];
 };
 
 struct Params {
   const uint8_t* stack;
   int64_t stack_vs;
+  int view_bytes;  // n_img * H * W (< 2^31): buffer-descriptor range of one view's stack
   const uint8_t* tex;
   int64_t tex_vs;
   const int32_t* in_col;
@@ -94,14 +92,19 @@ struct Params {
   int nc, nr, kc, kr;  // code bits and available bit planes (pairs)
   int mask_mode;
   int mode;
-  int dbg;  // measurement-only ablations (SLGPU_DEBUG): 1 = tile from blockIdx, 2 = no look-back
+  int dbg;  // measurement-only ablations (SLGPU_DEBUG): 1 = tile from blockIdx, 2 = no look-back,
+            // 4 = no f64 point math, 8 = no f32 point/no-point decision
   int Wp;
   const double4* planes;
+  const float4* planes32;  // f32 copies for the point/no-point pre-decision
   const double* xn;
   const double* yn;
+  const float* xn32;
+  const float* yn32;
   const double* nc_rays;
   double o0, o1, o2;
   const double* poses;
+  uint16_t* codes;  // [view][HW] packed records (ctx scratch)
   int32_t* col_out;
   int32_t* row_out;
   uint8_t* mask_out;
@@ -110,7 +113,8 @@ struct Params {
   int64_t* view_offsets;
   ViewStats* stats;
   unsigned* part;  // k_stats histogram replicas [view][kReps][kSlot]
-  unsigned long long* status;
+  int* tile_counts;          // k_decode -> k_scan
+  long long* tile_offsets;   // k_scan -> k_cloud
   Header* hdr;
 };
 
@@ -153,26 +157,8 @@ __device__ __forceinline__ uint32_t gray_to_binary(uint32_t g) {
   return g;
 }
 
-__device__ __forceinline__ unsigned long long ld_status(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void st_status(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int t = __shfl_up(v, d, 64);
-    if (lane >= d) v += t;
-  }
-  return v;
-}
-
 // --------------------------------------------------------------- k_stats ----
-// grid (bx <= kStatBlocks, n_views).  Clears k_decode's look-back words and
-// ticket; with the adaptive mask also builds, per view, the 256-bin histogram
+// grid (bx <= kStatBlocks, n_views).  Builds, per view, the 256-bin histogram
 // of the black plane and max(white - black):
 //   * per-wave LDS histograms, then no-return device atomics into one of
 //     kReps replicas of the view's histogram (blockIdx % kReps), so no more
@@ -181,15 +167,9 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 //     view's arrival counter; the block whose add is last reads (and zeroes)
 //     the replicas with returning atomics and evaluates numpy's float32
 //     percentile recipe.  The replicas are left zeroed for the next call.
-__global__ __launch_bounds__(kThreads) void k_stats(Params p, int64_t n_status, int do_stats,
-                                                    int vec) {
+__global__ __launch_bounds__(kThreads) void k_stats(Params p, int vec) {
   const int tid = threadIdx.x;
   const int view = blockIdx.y;
-  const int64_t lin = static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x;
-  const int64_t nblk = static_cast<int64_t>(gridDim.x) * gridDim.y;
-  for (int64_t i = lin * kThreads + tid; i < n_status; i += nblk * kThreads) p.status[i] = 0ull;
-  if (lin == 0 && tid == 0) p.hdr->ticket = 0u;
-  if (!do_stats) return;
 
   __shared__ unsigned sh[kWaves][256];
   __shared__ unsigned cdf[256];
@@ -328,6 +308,71 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p, int64_t n_status, 
 
 // -------------------------------------------------------------- k_decode ----
 
+// ------------------------------------------------------------------ layout ----
+// A workgroup (4 waves) owns a tile of kTile = 4096 pixels; wave w owns the
+// tile's pixels [w*1024, (w+1)*1024).
+//   streaming layout  : lane l holds 16 contiguous pixels -> 16-byte loads and
+//                       stores, fully coalesced;
+//   interleaved layout: in step k lane l holds pixel k*64 + l -> coalesced
+//                       table/plane gathers and per-pixel stores.
+// Per-wave LDS rows transpose one layout into the other.
+//
+// Pipeline (one stream): k_stats -> k_decode -> k_scan -> k_cloud.
+//   k_decode : Gray decode + mask + point/no-point decision; per-pixel 2-byte
+//              records and one point count per tile;
+//   k_scan   : exclusive scan of the tile counts (tile and view offsets);
+//   k_cloud  : exact f64 points written at their final, np.where-ordered
+//              positions.  No inter-workgroup waits anywhere.
+constexpr int kWavePx = 64 * kPx;
+
+// Is |n.r| > 1e-6 (sl_system.py:642) for the pixel at (u, v) / ray index q
+// whose clipped column code is c?  Decided in f32 with a rigorous error bound
+// B: the f32 rounding of the inputs, of the ray and of the dot product stay
+// below 2^-21 of S = sum|n_i r_i|, and B uses 2^-18.  Pixels within B of the
+// threshold are decided by the exact f64 reference arithmetic.
+__device__ __forceinline__ bool has_point(const Params& p, int mode, int c, int u, int v, int64_t q) {
+  const float4 pf = p.planes32[c];
+  float x, y, z, inv;
+  if (mode & M_NC) {
+    x = static_cast<float>(p.nc_rays[q]);
+    y = static_cast<float>(p.nc_rays[p.HW + q]);
+    z = static_cast<float>(p.nc_rays[2 * p.HW + q]);
+    inv = 1.0f;
+  } else {
+    x = p.xn32[u];
+    y = p.yn32[v];
+    z = 1.0f;
+    inv = __frsqrt_rn(x * x + y * y + 1.0f);
+  }
+  const float a = fabsf((pf.x * x + pf.y * y + pf.z * z) * inv);
+  const float S = (fabsf(pf.x * x) + fabsf(pf.y * y) + fabsf(pf.z * z)) * inv;
+  const float B = S * 3.814697265625e-06f;  // 2^-18
+  if (a > 1e-6f + B) return true;
+  if (a < 1e-6f - B) return false;
+  double r0, r1, r2;
+  if (mode & M_NC) {
+    r0 = p.nc_rays[q];
+    r1 = p.nc_rays[p.HW + q];
+    r2 = p.nc_rays[2 * p.HW + q];
+  } else {
+    const double xd = p.xn[u], yd = p.yn[v];
+    const double nrm = sqrt((xd * xd + yd * yd) + 1.0);
+    r0 = xd / nrm;
+    r1 = yd / nrm;
+    r2 = 1.0 / nrm;
+  }
+  const double4 pl = p.planes[c];
+  return fabs((pl.x * r0 + pl.y * r1) + pl.z * r2) > 1e-6;
+}
+
+// ================================================================ k_decode ====
+// gray_decode (sl_system.py:519-577): mask, column and row code of every
+// pixel, streaming the uint8 stack once (M_FROMMAPS: a caller's col_map + mask
+// instead).  Outputs by mode bit:
+//   M_MAPS  col/row int32 + mask u8 maps, full frame (what gray_decode returns);
+//   M_CODES record16 = min(col, Wp-1) | point << 15 per pixel (np.clip,
+//           sl_system.py:626; point = mask & |n.r| > 1e-6) and the tile's
+//           point count, for k_scan / k_cloud.
 template <int KC, int KR, int MODE, int VEC>
 __global__ __launch_bounds__(kThreads, 2) void k_decode(Params p) {
   constexpr bool kStatic = KC >= 0;
@@ -335,120 +380,291 @@ __global__ __launch_bounds__(kThreads, 2) void k_decode(Params p) {
   const int kc = KC >= 0 ? KC : p.kc;
   const int kr = KR >= 0 ? KR : p.kr;
   const int nc = p.nc, nr = p.nr;
+  const bool vload = VEC > 0;
 
-  __shared__ float s_xyz[3 * kTile + 8];
-  __shared__ uint32_t s_bgr[(3 * kTile + 8) / 4 + 2];
+  __shared__ uint32_t s_code[kWaves][kWavePx];  // col | row << 16
+  __shared__ uint8_t s_mask[kWaves][kWavePx];
   __shared__ int s_wsum[kWaves];
-  __shared__ unsigned s_tile;
-  __shared__ long long s_excl;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  if (tid == 0) s_tile = (p.dbg & 1) ? blockIdx.x : atomicAdd(&p.hdr->ticket, 1u);
-  __syncthreads();
-  const unsigned tile = s_tile;
-  const int view = static_cast<int>(tile / p.tiles_per_view);
-  const int64_t lt = tile - static_cast<int64_t>(view) * p.tiles_per_view;
-  const int64_t px0 = lt * kTile + static_cast<int64_t>(tid) * kPx;
-  const int n_px = static_cast<int>(min<int64_t>(max<int64_t>(p.HW - px0, 0), kPx));
-  const int64_t px_ld = n_px > 0 ? px0 : 0;  // keep loads unconditional and in bounds
-  const bool vload = VEC > 0;
+  const int64_t HW = p.HW;
+  const int view = static_cast<int>(blockIdx.x / p.tiles_per_view);
+  const int64_t lt = blockIdx.x - static_cast<int64_t>(view) * p.tiles_per_view;
 
-  uint32_t codec[kPx], coder[kPx];
-  unsigned valid = 0u;  // bit k: pixel k passes the shadow/contrast mask
-  uint4 tq0 = make_uint4(0, 0, 0, 0), tq1 = tq0, tq2 = tq0;
-
-  if (!(mode & M_FROMMAPS)) {
-    const uint8_t* src = p.stack + view * p.stack_vs + px_ld;
-    const int64_t HW = p.HW;
-    const uint4 wq = ld16(src, n_px, vload);
-    const uint4 bq = ld16(src + HW, n_px, vload);
-    if ((mode & M_CLOUD) && p.tex != nullptr) {
-      const uint8_t* t = p.tex + view * p.tex_vs + 3 * px_ld;
+  // ======================= A) streaming layout =======================
+  {
+    const int64_t px0 = lt * kTile + static_cast<int64_t>(tid) * kPx;
+    const int n_px = static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx));
+    const int64_t px_ld = n_px > 0 ? px0 : 0;  // keep loads unconditional and in bounds
+    uint32_t* lc = &s_code[wid][lane * kPx];
+    uint8_t* lm = &s_mask[wid][lane * kPx];
+    if (mode & M_FROMMAPS) {
+      // reconstruct_point_cloud's inputs: col_map (clipped, sl_system.py:626) and mask
+      const int64_t o = view * HW + px_ld;
+      uint32_t col[kPx];
+      uint32_t mw[4] = {0u, 0u, 0u, 0u};
       if (vload) {
-        tq0 = reinterpret_cast<const uint4*>(t)[0];
-        tq1 = reinterpret_cast<const uint4*>(t)[1];
-        tq2 = reinterpret_cast<const uint4*>(t)[2];
+        const int4* cm = reinterpret_cast<const int4*>(p.in_col + o);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int4 v = cm[i];
+          col[4 * i] = v.x;
+          col[4 * i + 1] = v.y;
+          col[4 * i + 2] = v.z;
+          col[4 * i + 3] = v.w;
+        }
+        const uint4 mq = *reinterpret_cast<const uint4*>(p.in_mask + o);
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) mw[k >> 2] |= (byte_of(mq, k) != 0u && k < n_px) ? (1u << (8 * (k & 3))) : 0u;
       } else {
-        tq0 = ld16(t, 3 * n_px, false);
-        tq1 = ld16(t + 16, 3 * n_px - 16, false);
-        tq2 = ld16(t + 32, 3 * n_px - 32, false);
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) {
+          col[k] = k < n_px ? static_cast<uint32_t>(p.in_col[o + k]) : 0u;
+          mw[k >> 2] |= (k < n_px && p.in_mask[o + k] != 0) ? (1u << (8 * (k & 3))) : 0u;
+        }
       }
-    }
-    // ---- Gray bit planes: (pattern, inverse) pairs, columns then rows ----
-    const int krr = (mode & M_ROWS) ? kr : 0;
-    const int npl = 2 * (kc + krr);
-    uint32_t cA[4] = {0, 0, 0, 0}, cB[4] = {0, 0, 0, 0};
-    uint32_t rA[4] = {0, 0, 0, 0}, rB[4] = {0, 0, 0, 0};
-    uint4 ring[kRing];
-    const uint8_t* pat = src + 2 * HW;
 #pragma unroll
-    for (int j = 0; j < kRing; ++j)
-      if (j < npl) ring[j] = ld16(pat + j * HW, n_px, vload);
+      for (int w = 0; w < 4; ++w) {
+        uint32_t cw[4];
 #pragma unroll
-    for (int base = 0; base < (kStatic ? 2 * (KC + KR) : npl); base += kRing) {
+        for (int e = 0; e < 4; ++e)
+          cw[e] = static_cast<uint32_t>(min(max(static_cast<int>(col[4 * w + e]), 0), p.Wp - 1));
+        *reinterpret_cast<uint4*>(lc + 4 * w) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+        *reinterpret_cast<uint32_t*>(lm + 4 * w) = mw[w];
+      }
+    } else {
+      // Plane loads: on the vector path a buffer descriptor of the view's
+      // stack (SGPRs) + the lane's 32-bit pixel offset + the plane offset in an SGPR.
+      const uint8_t* vbase = p.stack + view * p.stack_vs;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vbase), 0, p.view_bytes, 0x00020000);
+      const int voff = static_cast<int>(px_ld);
+      auto ldp = [&](int plane) -> uint4 {
+        if (vload) {
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, plane * static_cast<int>(HW), 0);
+          return make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        return ld16(vbase + px_ld + static_cast<int64_t>(plane) * HW, n_px, false);
+      };
+      const uint4 wq = ldp(0);
+      const uint4 bq = ldp(1);
+      // ---- Gray bit planes: (pattern, inverse) pairs, columns then rows ----
+      const int krr = (mode & M_ROWS) ? kr : 0;
+      const int npl = 2 * (kc + krr);
+      uint32_t cA[4] = {0, 0, 0, 0}, cB[4] = {0, 0, 0, 0};
+      uint32_t rA[4] = {0, 0, 0, 0}, rB[4] = {0, 0, 0, 0};
+      // Fold one (pattern, inverse) pair into per-byte-lane accumulators:
+      // acc = (acc << 1) | bit holds at most 8 bits per byte lane, so no carry
+      // crosses into the neighbouring pixel; codes of up to 16 bits use A then B.
+      auto consume = [&](const uint4& P, const uint4& I, int pair) {
+        uint32_t m[4];
 #pragma unroll
-      for (int j = 0; j < kRing; j += 2) {
-        const int pl = base + j;
-        if (pl < npl) {
-          const uint4 P = ring[j];
-          const uint4 I = ring[j + 1];
-          if (pl + kRing < npl) {
-            ring[j] = ld16(pat + (pl + kRing) * HW, n_px, vload);
-            ring[j + 1] = ld16(pat + (pl + kRing + 1) * HW, n_px, vload);
-          }
-          const int pair = pl >> 1;
-          uint32_t m[4];
+        for (int w = 0; w < 4; ++w) m[w] = gt_msb(word(P, w), word(I, w)) >> 7;
+        if (pair < kc) {
+          if (pair < 8) {
 #pragma unroll
-          for (int w = 0; w < 4; ++w) m[w] = gt_msb(word(P, w), word(I, w)) >> 7;
-          // acc = (acc << 1) | bit: at most 8 bits per byte lane, so no carry
-          // crosses into the neighbouring pixel.
-          if (pair < kc) {
-            if (pair < 8) {
-#pragma unroll
-              for (int w = 0; w < 4; ++w) cA[w] = (cA[w] << 1) | m[w];
-            } else {
-#pragma unroll
-              for (int w = 0; w < 4; ++w) cB[w] = (cB[w] << 1) | m[w];
-            }
-          } else if (pair - kc < 8) {
-#pragma unroll
-            for (int w = 0; w < 4; ++w) rA[w] = (rA[w] << 1) | m[w];
+            for (int w = 0; w < 4; ++w) cA[w] = (cA[w] << 1) | m[w];
           } else {
 #pragma unroll
-            for (int w = 0; w < 4; ++w) rB[w] = (rB[w] << 1) | m[w];
+            for (int w = 0; w < 4; ++w) cB[w] = (cB[w] << 1) | m[w];
+          }
+        } else if (pair - kc < 8) {
+#pragma unroll
+          for (int w = 0; w < 4; ++w) rA[w] = (rA[w] << 1) | m[w];
+        } else {
+#pragma unroll
+          for (int w = 0; w < 4; ++w) rB[w] = (rB[w] << 1) | m[w];
+        }
+      };
+      if (kStatic) {
+        // fully unrolled: every plane load issues up front (the widest
+        // memory-level parallelism a wave can have)
+#pragma unroll
+        for (int pr = 0; pr < KC + KR; ++pr)
+          if (pr < kc + krr) consume(ldp(2 + 2 * pr), ldp(3 + 2 * pr), pr);
+      } else {
+        uint4 ring[kRing];
+#pragma unroll
+        for (int j = 0; j < kRing; ++j)
+          if (j < npl) ring[j] = ldp(2 + j);
+        for (int base = 0; base < npl; base += kRing) {
+#pragma unroll
+          for (int j = 0; j < kRing; j += 2) {
+            const int pl = base + j;
+            if (pl < npl) {
+              const uint4 P = ring[j];
+              const uint4 I = ring[j + 1];
+              if (pl + kRing < npl) {
+                ring[j] = ldp(2 + pl + kRing);
+                ring[j + 1] = ldp(3 + pl + kRing);
+              }
+              consume(P, I, pl >> 1);
+            }
           }
         }
       }
-    }
-    // ---- mask + Gray -> binary ----
-    int thr_w, thr_c;
-    if (p.mask_mode == SL_MASK_FIXED) {
-      thr_w = 40;
-      thr_c = 10;
-    } else {
-      thr_w = p.stats[view].thr_white;
-      thr_c = p.stats[view].thr_contrast;
-    }
-    const int cBn = kc > 8 ? kc - 8 : 0;
-    const int rBn = krr > 8 ? krr - 8 : 0;
-    const int cSh = nc - kc;
-    const int rSh = nr - krr;
+      // ---- mask + Gray -> binary ----
+      int thr_w, thr_c;
+      if (p.mask_mode == SL_MASK_FIXED) {
+        thr_w = 40;
+        thr_c = 10;
+      } else {
+        thr_w = p.stats[view].thr_white;
+        thr_c = p.stats[view].thr_contrast;
+      }
+      const int cBn = kc > 8 ? kc - 8 : 0;
+      const int rBn = krr > 8 ? krr - 8 : 0;
+      const int cSh = nc - kc;
+      const int rSh = nr - krr;
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      const int w = k >> 2, s = 8 * (k & 3);
-      const uint32_t gc = (((cA[w] >> s) & 0xffu) << cBn) | ((cB[w] >> s) & 0xffu);
-      const uint32_t gr = (((rA[w] >> s) & 0xffu) << rBn) | ((rB[w] >> s) & 0xffu);
-      codec[k] = gray_to_binary(gc << cSh);
-      coder[k] = (mode & M_ROWS) ? gray_to_binary(gr << rSh) : 0u;
-      const int wv = static_cast<int>(byte_of(wq, k));
-      const int bv = static_cast<int>(byte_of(bq, k));
-      const bool ok = (k < n_px) && (wv > thr_w) && (wv - bv > thr_c);
-      valid |= ok ? (1u << k) : 0u;
+      for (int w = 0; w < 4; ++w) {
+        uint32_t cw[4];
+        uint32_t mw = 0u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = 4 * w + e, sft = 8 * e;
+          const uint32_t gc = (((cA[w] >> sft) & 0xffu) << cBn) | ((cB[w] >> sft) & 0xffu);
+          const uint32_t gr = (((rA[w] >> sft) & 0xffu) << rBn) | ((rB[w] >> sft) & 0xffu);
+          const uint32_t col = gray_to_binary(gc << cSh);
+          const uint32_t row = (mode & M_ROWS) ? gray_to_binary(gr << rSh) : 0u;
+          const int wv = static_cast<int>(byte_of(wq, k));
+          const int bv = static_cast<int>(byte_of(bq, k));
+          const uint32_t ok = ((k < n_px) && (wv > thr_w) && (wv - bv > thr_c)) ? 1u : 0u;
+          cw[e] = col | (row << 16);
+          mw |= ok << sft;
+        }
+        *reinterpret_cast<uint4*>(lc + 4 * w) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+        *reinterpret_cast<uint32_t*>(lm + 4 * w) = mw;
+      }
     }
-    if ((mode & M_CLOUD) && p.tex == nullptr) {
-      // BGR of 16 pixels = white bytes x3, packed like a [16][3] texture row
+  }
+  __syncthreads();
+
+  // ======================= B) interleaved layout =======================
+  const int64_t wpx = lt * kTile + static_cast<int64_t>(wid) * kWavePx + lane;  // step-0 pixel
+  const int64_t o = view * HW;
+  if (mode & M_MAPS) {
+#pragma unroll 4
+    for (int k = 0; k < kPx; ++k) {
+      const int64_t q = wpx + 64 * k;
+      if (q < HW) {
+        const uint32_t cw = s_code[wid][64 * k + lane];
+        p.col_out[o + q] = static_cast<int32_t>(cw & 0xffffu);
+        p.row_out[o + q] = static_cast<int32_t>(cw >> 16);
+        p.mask_out[o + q] = s_mask[wid][64 * k + lane];
+      }
+    }
+  }
+  if (!(mode & M_CODES)) return;
+  const int W = p.W;
+  int v = static_cast<int>(min<int64_t>(wpx, HW - 1) / W);
+  int u = static_cast<int>(min<int64_t>(wpx, HW - 1) - static_cast<int64_t>(v) * W);
+  int total_w = 0;
+#pragma unroll 4
+  for (int k = 0; k < kPx; ++k) {
+    const int64_t q = wpx + 64 * k;
+    const int c = static_cast<int>(min(s_code[wid][64 * k + lane] & 0xffffu, static_cast<uint32_t>(p.Wp - 1)));
+    const bool pt = s_mask[wid][64 * k + lane] && has_point(p, mode, c, u, v, min<int64_t>(q, HW - 1));
+    total_w += __popcll(__ballot(pt));
+    if (q < HW) p.codes[o + q] = static_cast<uint16_t>(c | (pt ? 0x8000 : 0));
+    u += 64;
+    while (u >= W) {
+      u -= W;
+      v = min(v + 1, p.H - 1);
+    }
+  }
+  if (lane == 0) s_wsum[wid] = total_w;
+  __syncthreads();
+  if (tid == 0) {
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) t += s_wsum[w];
+    p.tile_counts[blockIdx.x] = t;
+  }
+}
+
+// ================================================================== k_scan ====
+// Exclusive scan of the per-tile point counts (tiles of all views in order):
+// tile_offsets[t] = points before tile t; view_offsets[v] = points before view
+// v, view_offsets[V] = total.  One workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void k_scan(Params p) {
+  __shared__ long long s_part[1024];
+  const int tid = threadIdx.x;
+  const int64_t n = static_cast<int64_t>(p.n_views) * p.tiles_per_view;
+  const int64_t per = (n + 1023) / 1024;
+  const int64_t lo = min<int64_t>(tid * per, n), hi = min<int64_t>(lo + per, n);
+  long long s = 0;
+  for (int64_t i = lo; i < hi; ++i) s += p.tile_counts[i];
+  s_part[tid] = s;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // inclusive scan of the chunk sums
+    const long long t = tid >= d ? s_part[tid - d] : 0ll;
+    __syncthreads();
+    s_part[tid] += t;
+    __syncthreads();
+  }
+  long long run = tid ? s_part[tid - 1] : 0ll;
+  for (int64_t i = lo; i < hi; ++i) {
+    if (p.view_offsets && i % p.tiles_per_view == 0) p.view_offsets[i / p.tiles_per_view] = run;
+    p.tile_offsets[i] = run;
+    run += p.tile_counts[i];
+  }
+  if (tid == 1023 && p.view_offsets) p.view_offsets[p.n_views] = s_part[1023];
+}
+
+// ================================================================= k_cloud ====
+// reconstruct_point_cloud's arithmetic (sl_system.py:584-653) for the pixels
+// k_decode marked: exact f64 in the reference's operation order, stored at
+// tile offset + rank, i.e. in np.where order across tiles and views
+// (sl_system.py:601).
+template <int MODE, int VEC>
+__global__ __launch_bounds__(kThreads, 2) void k_cloud(Params p) {
+  const int mode = MODE >= 0 ? MODE : p.mode;
+  const bool vload = VEC > 0;
+
+  __shared__ uint32_t s_code[kWaves][kWavePx];  // record16
+  __shared__ uint32_t s_aux[kWaves][kWavePx];   // B | G << 8 | R << 16
+  __shared__ int s_wsum[kWaves];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int64_t HW = p.HW;
+  const int view = static_cast<int>(blockIdx.x / p.tiles_per_view);
+  const int64_t lt = blockIdx.x - static_cast<int64_t>(view) * p.tiles_per_view;
+
+  // ============ A) streaming layout: records + colour -> LDS rows ============
+  {
+    const int64_t px0 = lt * kTile + static_cast<int64_t>(tid) * kPx;
+    const int n_px = static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx));
+    const int64_t px_ld = n_px > 0 ? px0 : 0;
+    const uint16_t* src = p.codes + view * HW + px_ld;
+    uint32_t d[kPx / 2];
+    if (vload) {
+      const uint4 a = reinterpret_cast<const uint4*>(src)[0];
+      const uint4 b = reinterpret_cast<const uint4*>(src)[1];
+      d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+      d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < kPx / 2; ++i) {
+        const uint32_t lo = (2 * i < n_px) ? src[2 * i] : 0u;
+        const uint32_t hi = (2 * i + 1 < n_px) ? src[2 * i + 1] : 0u;
+        d[i] = lo | (hi << 16);
+      }
+    }
+    // colour: BGR texture, or the white plane replicated (the colour imread of
+    // a single-channel file 0, sl_system.py:580)
+    uint4 tq[3];
+    if (p.tex != nullptr) {
+      const uint8_t* t = p.tex + view * p.tex_vs + 3 * px_ld;
+      tq[0] = ld16(t, 3 * n_px, vload);
+      tq[1] = ld16(t + 16, 3 * n_px - 16, vload);
+      tq[2] = ld16(t + 32, 3 * n_px - 32, vload);
+    } else {
+      const uint4 wq = ld16(p.stack + view * p.stack_vs + px_ld, n_px, vload);
       uint32_t t[12];
 #pragma unroll
       for (int i = 0; i < 12; ++i) t[i] = 0u;
@@ -456,277 +672,139 @@ __global__ __launch_bounds__(kThreads, 2) void k_decode(Params p) {
       for (int k = 0; k < kPx; ++k) {
         const uint32_t wv = byte_of(wq, k);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const int b = 3 * k + c;
-          t[b >> 2] |= wv << (8 * (b & 3));
-        }
+        for (int c = 0; c < 3; ++c) t[(3 * k + c) >> 2] |= wv << (8 * ((3 * k + c) & 3));
       }
-      tq0 = make_uint4(t[0], t[1], t[2], t[3]);
-      tq1 = make_uint4(t[4], t[5], t[6], t[7]);
-      tq2 = make_uint4(t[8], t[9], t[10], t[11]);
+      tq[0] = make_uint4(t[0], t[1], t[2], t[3]);
+      tq[1] = make_uint4(t[4], t[5], t[6], t[7]);
+      tq[2] = make_uint4(t[8], t[9], t[10], t[11]);
     }
-    // ---- maps ----
-    if (mode & M_MAPS) {
-      const int64_t o = view * p.HW + px0;
-      if (vload && n_px == kPx) {
-        int4* cm = reinterpret_cast<int4*>(p.col_out + o);
-        int4* rm = reinterpret_cast<int4*>(p.row_out + o);
+    uint32_t* lc = &s_code[wid][lane * kPx];
+    uint32_t* la = &s_aux[wid][lane * kPx];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          cm[i] = make_int4(codec[4 * i], codec[4 * i + 1], codec[4 * i + 2], codec[4 * i + 3]);
-          rm[i] = make_int4(coder[4 * i], coder[4 * i + 1], coder[4 * i + 2], coder[4 * i + 3]);
-        }
-        uint32_t mw[4] = {0, 0, 0, 0};
+    for (int w = 0; w < 4; ++w) {
+      uint32_t aw[4], cw[4];
 #pragma unroll
-        for (int k = 0; k < kPx; ++k) mw[k >> 2] |= ((valid >> k) & 1u) << (8 * (k & 3));
-        *reinterpret_cast<uint4*>(p.mask_out + o) = make_uint4(mw[0], mw[1], mw[2], mw[3]);
-      } else {
+      for (int e = 0; e < 4; ++e) {
+        const int k = 4 * w + e, b = 3 * k;
+        aw[e] = byte_of(tq[b >> 4], b & 15) | (byte_of(tq[(b + 1) >> 4], (b + 1) & 15) << 8) |
+                (byte_of(tq[(b + 2) >> 4], (b + 2) & 15) << 16);
+        cw[e] = (k < n_px) ? ((d[k >> 1] >> (16 * (k & 1))) & 0xffffu) : 0u;
+      }
+      *reinterpret_cast<uint4*>(lc + 4 * w) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+      *reinterpret_cast<uint4*>(la + 4 * w) = make_uint4(aw[0], aw[1], aw[2], aw[3]);
+    }
+  }
+  __syncthreads();
+
+  // ============ B) interleaved layout: pixel k*64 + lane of the wave ============
+  // ranks: bit k of `mine` = this lane's pixel is a point; rel[k] = its rank
+  // among the wave's points of steps <= k; bit k of `steps` = step k has one.
+  unsigned mine = 0u, steps = 0u;
+  uint32_t rel[kPx];
+  int total_w = 0;
 #pragma unroll
-        for (int k = 0; k < kPx; ++k) {
-          if (k < n_px) {
-            p.col_out[o + k] = static_cast<int32_t>(codec[k]);
-            p.row_out[o + k] = static_cast<int32_t>(coder[k]);
-            p.mask_out[o + k] = static_cast<uint8_t>((valid >> k) & 1u);
+  for (int k = 0; k < kPx; ++k) {
+    const bool pt = (s_code[wid][64 * k + lane] >> 15) & 1u;
+    const unsigned long long m = __ballot(pt);
+    rel[k] = static_cast<uint32_t>(total_w) +
+             __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                       __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+    mine |= pt ? (1u << k) : 0u;
+    steps |= m ? (1u << k) : 0u;
+    total_w += __popcll(m);
+  }
+  if (lane == 0) s_wsum[wid] = total_w;
+  __syncthreads();
+  long long base = p.tile_offsets[blockIdx.x];
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) base += (w < wid) ? s_wsum[w] : 0;
+
+  // r = (x, y, 1) / sqrt((x*x + y*y) + 1) (sl_system.py:614-621), plane of the
+  // clipped code (:624-633), den = (n0 r0 + n1 r1) + n2 r2 (:638),
+  // t = -(n.Oc + d) / den (:639, :643), P = Oc + r t (:648); optional pose.
+  // Four steps at a time are computed branch-free so their chains interleave.
+  const int64_t wpx = lt * kTile + static_cast<int64_t>(wid) * kWavePx + lane;
+  const int W = p.W;
+  int v = static_cast<int>(min<int64_t>(wpx, HW - 1) / W);
+  int u = static_cast<int>(min<int64_t>(wpx, HW - 1) - static_cast<int64_t>(v) * W);
+  const double* pose = p.poses ? p.poses + 16 * view : nullptr;
+#pragma unroll
+  for (int g = 0; g < kPx; g += 4) {
+    if (((steps >> g) & 0xfu) != 0u && !(p.dbg & 4)) {
+      double X[4], Y[4], Z[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = g + e;
+        int uu = u, vv = v;
+#pragma unroll
+        for (int s = 0; s < e; ++s) {
+          uu += 64;
+          while (uu >= W) {
+            uu -= W;
+            vv = min(vv + 1, p.H - 1);
           }
         }
-      }
-    }
-  } else {
-    // ---- reconstruct_point_cloud on given maps ----
-    const int64_t o = view * p.HW + px_ld;
-    const uint8_t* t = p.tex + view * p.tex_vs + 3 * px_ld;
-    if (vload) {
-      const int4* cm = reinterpret_cast<const int4*>(p.in_col + o);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int4 v = cm[i];
-        codec[4 * i] = v.x;
-        codec[4 * i + 1] = v.y;
-        codec[4 * i + 2] = v.z;
-        codec[4 * i + 3] = v.w;
-      }
-      const uint4 mq = *reinterpret_cast<const uint4*>(p.in_mask + o);
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) valid |= (byte_of(mq, k) != 0u && k < n_px) ? (1u << k) : 0u;
-      tq0 = reinterpret_cast<const uint4*>(t)[0];
-      tq1 = reinterpret_cast<const uint4*>(t)[1];
-      tq2 = reinterpret_cast<const uint4*>(t)[2];
-    } else {
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) {
-        codec[k] = k < n_px ? static_cast<uint32_t>(p.in_col[o + k]) : 0u;
-        valid |= (k < n_px && p.in_mask[o + k] != 0) ? (1u << k) : 0u;
-      }
-      tq0 = ld16(t, 3 * n_px, false);
-      tq1 = ld16(t + 16, 3 * n_px - 16, false);
-      tq2 = ld16(t + 32, 3 * n_px - 32, false);
-    }
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) coder[k] = 0u;
-  }
-
-  if (!(mode & M_CLOUD)) return;
-
-  // ---- ray / plane intersection, f64 in the reference's operation order ----
-  float fx_[kPx], fy_[kPx], fz_[kPx];
-  double dx_[kPx], dy_[kPx], dz_[kPx];
-  unsigned pts = 0u;
-  {
-    int v = static_cast<int>(px0 / p.W);
-    int u = static_cast<int>(px0 - static_cast<int64_t>(v) * p.W);
-    const double* pose = p.poses ? p.poses + 16 * view : nullptr;
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      dx_[k] = dy_[k] = dz_[k] = 0.0;
-      fx_[k] = fy_[k] = fz_[k] = 0.0f;
-      if (valid & (1u << k)) {
         double r0, r1, r2;
         if (mode & M_NC) {
-          const int64_t q = px0 + k;
+          const int64_t q = min<int64_t>(wpx + 64 * k, HW - 1);
           r0 = p.nc_rays[q];
-          r1 = p.nc_rays[p.HW + q];
-          r2 = p.nc_rays[2 * p.HW + q];
+          r1 = p.nc_rays[HW + q];
+          r2 = p.nc_rays[2 * HW + q];
         } else {
-          const double x = p.xn[u];
-          const double y = p.yn[v];
-          // np.linalg.norm(rays, axis=0): sqrt((x*x + y*y) + 1*1)
+          const double x = p.xn[uu];
+          const double y = p.yn[vv];
           const double nrm = sqrt((x * x + y * y) + 1.0);
           r0 = x / nrm;
           r1 = y / nrm;
           r2 = 1.0 / nrm;
         }
-        // np.clip(c, 0, Wp-1) (sl_system.py:626)
-        const int c = min(max(static_cast<int>(codec[k]), 0), p.Wp - 1);
-        const double4 pl = p.planes[c];
+        const double4 pl = p.planes[s_code[wid][64 * k + lane] & 0x7fffu];
         const double den = (pl.x * r0 + pl.y * r1) + pl.z * r2;
-        if (fabs(den) > 1e-6) {
-          const double num = ((pl.x * p.o0 + pl.y * p.o1) + pl.z * p.o2) + pl.w;
-          const double t = -num / den;
-          double X = p.o0 + r0 * t;
-          double Y = p.o1 + r1 * t;
-          double Z = p.o2 + r2 * t;
-          if (pose) {
-            const double X2 = ((pose[0] * X + pose[1] * Y) + pose[2] * Z) + pose[3];
-            const double Y2 = ((pose[4] * X + pose[5] * Y) + pose[6] * Z) + pose[7];
-            const double Z2 = ((pose[8] * X + pose[9] * Y) + pose[10] * Z) + pose[11];
-            X = X2;
-            Y = Y2;
-            Z = Z2;
-          }
+        const double num = ((pl.x * p.o0 + pl.y * p.o1) + pl.z * p.o2) + pl.w;
+        const double t = -num / den;
+        X[e] = p.o0 + r0 * t;
+        Y[e] = p.o1 + r1 * t;
+        Z[e] = p.o2 + r2 * t;
+        if (pose) {
+          const double X2 = ((pose[0] * X[e] + pose[1] * Y[e]) + pose[2] * Z[e]) + pose[3];
+          const double Y2 = ((pose[4] * X[e] + pose[5] * Y[e]) + pose[6] * Z[e]) + pose[7];
+          const double Z2 = ((pose[8] * X[e] + pose[9] * Y[e]) + pose[10] * Z[e]) + pose[11];
+          X[e] = X2;
+          Y[e] = Y2;
+          Z[e] = Z2;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = g + e;
+        if ((mine >> k) & 1u) {
+          const long long o = base + rel[k];
           if (mode & M_XYZ64) {
-            dx_[k] = X;
-            dy_[k] = Y;
-            dz_[k] = Z;
+            double* xyz = static_cast<double*>(p.xyz) + 3 * o;
+            xyz[0] = X[e];
+            xyz[1] = Y[e];
+            xyz[2] = Z[e];
           } else {
-            fx_[k] = static_cast<float>(X);
-            fy_[k] = static_cast<float>(Y);
-            fz_[k] = static_cast<float>(Z);
+            float* xyz = static_cast<float*>(p.xyz) + 3 * o;
+            xyz[0] = static_cast<float>(X[e]);
+            xyz[1] = static_cast<float>(Y[e]);
+            xyz[2] = static_cast<float>(Z[e]);
           }
-          pts |= 1u << k;
+          const uint32_t aux = s_aux[wid][64 * k + lane];
+          uint8_t* cc = p.bgr + 3 * o;
+          cc[0] = static_cast<uint8_t>(aux);
+          cc[1] = static_cast<uint8_t>(aux >> 8);
+          cc[2] = static_cast<uint8_t>(aux >> 16);
         }
       }
-      if (++u == p.W) {
-        u = 0;
-        ++v;
-      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-  }
-
-  // ---- workgroup scan of point counts ----
-  const int cnt = __popc(pts);
-  const int incl = wave_incl_scan(cnt, lane);
-  if (lane == 63) s_wsum[wid] = incl;
-  __syncthreads();
-  int woff = 0, total = 0;
 #pragma unroll
-  for (int w = 0; w < kWaves; ++w) {
-    const int s = s_wsum[w];
-    woff += (w < wid) ? s : 0;
-    total += s;
-  }
-  const int off = woff + incl - cnt;
-
-  // ---- stage f32 points + colours in LDS (pixel order) ----
-  uint8_t* sb = reinterpret_cast<uint8_t*>(s_bgr);
-  {
-    int o = off;
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      if (pts & (1u << k)) {
-        if (!(mode & M_XYZ64)) {
-          s_xyz[3 * o + 0] = fx_[k];
-          s_xyz[3 * o + 1] = fy_[k];
-          s_xyz[3 * o + 2] = fz_[k];
-        }
-        const int b = 3 * k;
-        sb[3 * o + 0] = static_cast<uint8_t>(byte_of(b < 16 ? tq0 : b < 32 ? tq1 : tq2, b & 15));
-        sb[3 * o + 1] = static_cast<uint8_t>(
-            byte_of((b + 1) < 16 ? tq0 : (b + 1) < 32 ? tq1 : tq2, (b + 1) & 15));
-        sb[3 * o + 2] = static_cast<uint8_t>(
-            byte_of((b + 2) < 16 ? tq0 : (b + 2) < 32 ? tq1 : tq2, (b + 2) & 15));
-        ++o;
-      }
-    }
-  }
-
-  // ---- decoupled look-back over tiles in ticket order (wave 0) ----
-  if (wid == 0) {
-    unsigned long long* st = p.status;
-    if (lane == 0) st_status(st + tile, (tile == 0 ? kFlagPre : kFlagAgg) | static_cast<unsigned long long>(total));
-    long long excl = (p.dbg & 2) ? static_cast<long long>(tile) * kTile : 0;
-    if (tile > 0 && !(p.dbg & 2)) {
-      long long j = static_cast<long long>(tile) - 1;
-      unsigned spins = 0;
-      for (;;) {
-        const long long idx = j - lane;
-        const unsigned long long s = idx >= 0 ? ld_status(st + idx) : kFlagPre;
-        const unsigned long long flag = s & ~kValMask;
-        const unsigned long long pre = __ballot(flag == kFlagPre);
-        const unsigned long long zero = __ballot(flag == 0ull);
-        const int lp = pre ? __ffsll(static_cast<long long>(pre)) - 1 : 64;
-        const unsigned long long before = lp >= 64 ? ~0ull : ((1ull << lp) - 1ull) | (1ull << lp);
-        if (zero & before) {
-          if (++spins > kSpinLimit) {
-            if (lane == 0) atomicOr(&p.hdr->error, 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        long long v = (lane <= lp) ? static_cast<long long>(s & kValMask) : 0ll;
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-        excl += v;
-        if (lp < 64) break;
-        j -= 64;
-      }
-      if (lane == 0) st_status(st + tile, kFlagPre | static_cast<unsigned long long>(excl + total));
-    }
-    if (lane == 0) {
-      s_excl = excl;
-      if (p.view_offsets) {
-        if (lt == 0) p.view_offsets[view] = excl;
-        if (tile + 1u == static_cast<unsigned>(p.n_views) * p.tiles_per_view)
-          p.view_offsets[p.n_views] = excl + total;
-      }
-    }
-  }
-  __syncthreads();
-  const long long E = s_excl;
-
-  if (mode & M_XYZ64) {
-    double* xyz = static_cast<double*>(p.xyz);
-    int o = off;
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      if (pts & (1u << k)) {
-        const long long g = 3 * (E + o);
-        xyz[g] = dx_[k];
-        xyz[g + 1] = dy_[k];
-        xyz[g + 2] = dz_[k];
-        ++o;
-      }
-    }
-  } else {
-    // floats [3E, 3E + 3T) from s_xyz[0 ..): aligned 16-B chunks of the
-    // destination, element stores at the ragged ends.
-    float* xyz = static_cast<float*>(p.xyz);
-    const long long g_lo = 3 * E, g_hi = 3 * (E + total);
-    const long long gbase = g_lo & ~3ll;
-    const int nchunk = static_cast<int>((g_hi - gbase + 3) >> 2);
-    for (int c = tid; c < nchunk; c += kThreads) {
-      const long long g0 = gbase + 4ll * c;
-      const int l0 = static_cast<int>(g0 - g_lo);
-      if (g0 >= g_lo && g0 + 4 <= g_hi) {
-        *reinterpret_cast<float4*>(xyz + g0) =
-            make_float4(s_xyz[l0], s_xyz[l0 + 1], s_xyz[l0 + 2], s_xyz[l0 + 3]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (g0 + e >= g_lo && g0 + e < g_hi) xyz[g0 + e] = s_xyz[l0 + e];
-      }
-    }
-  }
-  {
-    // colour bytes [3E, 3E + 3T) from sb[0 ..)
-    const long long h_lo = 3 * E, h_hi = 3 * (E + total);
-    const long long hbase = h_lo & ~15ll;
-    const int nchunk = static_cast<int>((h_hi - hbase + 15) >> 4);
-    for (int c = tid; c < nchunk; c += kThreads) {
-      const long long h0 = hbase + 16ll * c;
-      const int l0 = static_cast<int>(h0 - h_lo);
-      if (h0 >= h_lo && h0 + 16 <= h_hi) {
-        const int a = l0 >> 2, sh = l0 & 3;
-        uint32_t d[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) d[i] = s_bgr[a + i];
-        uint32_t o4[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o4[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-        *reinterpret_cast<uint4*>(p.bgr + h0) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
-      } else {
-        for (int e = 0; e < 16; ++e)
-          if (h0 + e >= h_lo && h0 + e < h_hi) p.bgr[h0 + e] = sb[l0 + e];
+    for (int s = 0; s < 4; ++s) {
+      u += 64;
+      while (u >= W) {
+        u -= W;
+        v = min(v + 1, p.H - 1);
       }
     }
   }
@@ -746,6 +824,7 @@ struct sl_ctx {
   double* d_planes = nullptr;
   double* d_xn = nullptr;
   double* d_yn = nullptr;
+  float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H]
   double* d_nc = nullptr;
   // scratch
   Header* d_hdr = nullptr;
@@ -753,12 +832,16 @@ struct sl_ctx {
   int64_t cap_views = 0;
   unsigned* d_part = nullptr;
   int64_t cap_part = 0;
-  unsigned long long* d_status = nullptr;
-  int64_t cap_status = 0;
+  int* d_tile_counts = nullptr;
+  int64_t cap_tc = 0;
+  long long* d_tile_offsets = nullptr;
+  int64_t cap_to = 0;
+  uint16_t* d_codes = nullptr;  // k_decode -> k_cloud records
+  int64_t cap_codes = 0;
   int last_views = 0;
   int dbg = 0;
-  // optional per-launch HIP-event timing of k_stats / k_decode
-  std::vector<hipEvent_t> prof_ev;  // 3 events per launch slot
+  // optional per-launch HIP-event timing of k_stats / k_decode / k_cloud
+  std::vector<hipEvent_t> prof_ev;  // kProfEv events per launch slot
   int prof_n = 0;
 };
 
@@ -799,67 +882,88 @@ int ensure_scratch(sl_ctx* c, int64_t views, int64_t tiles) {
   if (r) return r;
   r = grow(c, &c->d_part, &c->cap_part, views * kReps * kSlot);
   if (r) return r;
-  return grow(c, &c->d_status, &c->cap_status, tiles);
+  r = grow(c, &c->d_tile_counts, &c->cap_tc, tiles);
+  if (r) return r;
+  return grow(c, &c->d_tile_offsets, &c->cap_to, tiles);
 }
 
 using KernelFn = void (*)(Params);
+constexpr int kProfEv = 4;  // events per launch: before k_stats, k_decode, k_cloud, after
 
-template <int KC, int KR, int MODE>
-KernelFn pick_static() {
-  return k_decode<KC, KR, MODE, 1>;
-}
-
-KernelFn pick_kernel(int kc, int kr, int mode, bool vec) {
-  // Specialisations for the benchmark configurations (all unaligned, Nc, f64
-  // or from-map calls go to the generic instantiation).
-  if (vec && !(mode & (M_XYZ64 | M_FROMMAPS | M_NC))) {
-    const int m = mode;
-    const int maps_cloud = M_MAPS | M_CLOUD | M_ROWS;
-    if (m == maps_cloud && kc == 11 && kr == 11) return pick_static<11, 11, M_MAPS | M_CLOUD | M_ROWS>();
-    if (m == maps_cloud && kc == 10 && kr == 10) return pick_static<10, 10, M_MAPS | M_CLOUD | M_ROWS>();
-    if (m == maps_cloud && kc == 10 && kr == 0) return pick_static<10, 0, M_MAPS | M_CLOUD | M_ROWS>();
-    if (m == M_CLOUD && kc == 11) return pick_static<11, 0, M_CLOUD>();
-    if (m == M_CLOUD && kc == 10) return pick_static<10, 0, M_CLOUD>();
-    if (m == (M_MAPS | M_ROWS) && kc == 11 && kr == 11) return pick_static<11, 11, M_MAPS | M_ROWS>();
+// k_decode specialisations for the benchmark configurations; everything else
+// (other bit counts, unaligned frames) runs the generic instantiation.
+KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
+  if (vec && !(mode & (M_NC | M_FROMMAPS))) {
+    const int mr = M_MAPS | M_ROWS, mrc = M_MAPS | M_ROWS | M_CODES;
+    if (mode == mrc && kc == 11 && kr == 11) return k_decode<11, 11, mrc, 1>;
+    if (mode == mrc && kc == 10 && kr == 10) return k_decode<10, 10, mrc, 1>;
+    if (mode == mrc && kc == 10 && kr == 0) return k_decode<10, 0, mrc, 1>;
+    if (mode == mr && kc == 11 && kr == 11) return k_decode<11, 11, mr, 1>;
+    if (mode == M_CODES && kc == 11) return k_decode<11, 0, M_CODES, 1>;
+    if (mode == M_CODES && kc == 10) return k_decode<10, 0, M_CODES, 1>;
   }
   return vec ? k_decode<-1, -1, -1, 1> : k_decode<-1, -1, -1, 0>;
 }
 
+KernelFn pick_cloud(int mode, bool vec) {
+  if (vec && mode == 0) return k_cloud<0, 1>;  // f32 xyz, pinhole rays
+  return vec ? k_cloud<-1, 1> : k_cloud<-1, 0>;
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-int launch(sl_ctx* c, Params& p, bool vec, bool do_stats, hipStream_t s) {
+// Enqueue [k_stats] -> k_decode -> [k_scan -> k_cloud] on stream s.
+// cloud_mode < 0: no cloud.
+int launch(sl_ctx* c, Params& p, bool vec, bool do_stats, int decode_mode, int cloud_mode, hipStream_t s) {
   const int64_t tiles = static_cast<int64_t>(p.n_views) * p.tiles_per_view;
+  if (tiles >= (1ll << 31)) return fail(c, SL_EINVAL, "too many pixels in one call");
   int r = ensure_scratch(c, p.n_views, tiles);
   if (r) return r;
+  if (decode_mode & M_CODES) {
+    r = grow(c, &c->d_codes, &c->cap_codes, static_cast<int64_t>(p.n_views) * p.HW + 16);
+    if (r) return r;
+  }
   p.stats = c->d_stats;
   p.part = c->d_part;
-  p.status = c->d_status;
+  p.tile_counts = c->d_tile_counts;
+  p.tile_offsets = c->d_tile_offsets;
   p.hdr = c->d_hdr;
+  p.codes = c->d_codes;
   c->last_views = p.n_views;
-  // k_stats: enough blocks to cover the views with ~2K workgroups in total
-  int bx = 1;
+  hipEvent_t* ev = nullptr;
+  if (!c->prof_ev.empty() && kProfEv * (c->prof_n + 1) <= static_cast<int>(c->prof_ev.size()))
+    ev = &c->prof_ev[kProfEv * c->prof_n++];
+  if (ev) HIP_TRY(c, hipEventRecord(ev[0], s));
   if (do_stats) {
-    bx = static_cast<int>(std::max<int64_t>(
+    const int bx = static_cast<int>(std::max<int64_t>(
         1, std::min<int64_t>({static_cast<int64_t>(p.tiles_per_view), int64_t{kStatBlocks},
                               std::max<int64_t>(1, 2048 / p.n_views)})));
-  } else {
-    bx = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(64, (tiles + 255) / 256)));
+    int vec_flag = vec ? 1 : 0;
+    void* args[] = {&p, &vec_flag};
+    HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(k_stats), dim3(bx, p.n_views), dim3(kThreads), args,
+                               0, s));
   }
-  int stats_flag = do_stats ? 1 : 0, vec_flag = vec ? 1 : 0;
-  int64_t n_status = tiles;
-  void* sargs[] = {&p, &n_status, &stats_flag, &vec_flag};
-  hipEvent_t* ev = nullptr;
-  if (!c->prof_ev.empty() && 3 * (c->prof_n + 1) <= static_cast<int>(c->prof_ev.size()))
-    ev = &c->prof_ev[3 * c->prof_n++];
-  if (ev) HIP_TRY(c, hipEventRecord(ev[0], s));
-  HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(k_stats), dim3(bx, do_stats ? p.n_views : 1),
-                             dim3(kThreads), sargs, 0, s));
   if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
-  KernelFn fn = pick_kernel(p.kc, (p.mode & M_ROWS) ? p.kr : 0, p.mode, vec);
-  void* dargs[] = {&p};
-  HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(static_cast<unsigned>(tiles)),
-                             dim3(kThreads), dargs, 0, s));
+  {
+    Params q = p;
+    q.mode = decode_mode;
+    void* args[] = {&q};
+    KernelFn fn = pick_decode(q.kc, (decode_mode & M_ROWS) ? q.kr : 0, decode_mode, vec);
+    HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(static_cast<unsigned>(tiles)),
+                               dim3(kThreads), args, 0, s));
+  }
   if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
+  if (cloud_mode >= 0) {
+    void* sargs[] = {&p};
+    HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(k_scan), dim3(1), dim3(1024), sargs, 0, s));
+    Params q = p;
+    q.mode = cloud_mode;
+    void* args[] = {&q};
+    KernelFn fn = pick_cloud(cloud_mode, vec);
+    HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(static_cast<unsigned>(tiles)),
+                               dim3(kThreads), args, 0, s));
+  }
+  if (ev) HIP_TRY(c, hipEventRecord(ev[3], s));
   return SL_OK;
 }
 
@@ -892,8 +996,9 @@ void sl_ctx_destroy(sl_ctx* c) {
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (void* ptr : {static_cast<void*>(c->d_planes), static_cast<void*>(c->d_xn), static_cast<void*>(c->d_yn),
                     static_cast<void*>(c->d_nc), static_cast<void*>(c->d_hdr), static_cast<void*>(c->d_stats),
+                    static_cast<void*>(c->d_f32), static_cast<void*>(c->d_codes),
                     static_cast<void*>(c->d_part),
-                    static_cast<void*>(c->d_status)})
+                    static_cast<void*>(c->d_tile_counts), static_cast<void*>(c->d_tile_offsets)})
     if (ptr) (void)hipFree(ptr);
   delete c;
 }
@@ -911,6 +1016,7 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
   if (!c) return SL_EINVAL;
   if (H < 1 || W < 1 || Wp < 1 || !K || !Oc || !planes)
     return fail(c, SL_EINVAL, "sl_set_calib: bad arguments");
+  if (Wp > 32768) return fail(c, SL_EINVAL, "sl_set_calib: at most 32768 projector columns");
   HIP_TRY(c, hipSetDevice(c->device));
   const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
   // (x_v - cx) / fx and (y_v - cy) / fy with integer pixel coordinates
@@ -931,13 +1037,23 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
   }
   for (double* ptr : {c->d_planes, c->d_xn, c->d_yn, c->d_nc})
     if (ptr) HIP_TRY(c, hipFree(ptr));
+  if (c->d_f32) HIP_TRY(c, hipFree(c->d_f32));
   c->d_planes = c->d_xn = c->d_yn = c->d_nc = nullptr;
+  c->d_f32 = nullptr;
   HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_planes), sizeof(double) * 4 * Wp));
   HIP_TRY(c, hipMemcpy(c->d_planes, planes, sizeof(double) * 4 * Wp, hipMemcpyHostToDevice));
   HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_xn), sizeof(double) * W));
   HIP_TRY(c, hipMemcpy(c->d_xn, xn.data(), sizeof(double) * W, hipMemcpyHostToDevice));
   HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_yn), sizeof(double) * H));
   HIP_TRY(c, hipMemcpy(c->d_yn, yn.data(), sizeof(double) * H, hipMemcpyHostToDevice));
+  {
+    std::vector<float> f(4 * static_cast<size_t>(Wp) + W + H);
+    for (int i = 0; i < 4 * Wp; ++i) f[i] = static_cast<float>(planes[i]);
+    for (int u = 0; u < W; ++u) f[4 * Wp + u] = static_cast<float>(xn[u]);
+    for (int v = 0; v < H; ++v) f[4 * Wp + W + v] = static_cast<float>(yn[v]);
+    HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_f32), sizeof(float) * f.size()));
+    HIP_TRY(c, hipMemcpy(c->d_f32, f.data(), sizeof(float) * f.size(), hipMemcpyHostToDevice));
+  }
   if (use_nc) {
     HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_nc), sizeof(double) * 3 * HW));
     HIP_TRY(c, hipMemcpy(c->d_nc, Nc, sizeof(double) * 3 * HW, hipMemcpyHostToDevice));
@@ -977,6 +1093,9 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.planes = reinterpret_cast<const double4*>(c->d_planes);
   p.xn = c->d_xn;
   p.yn = c->d_yn;
+  p.planes32 = reinterpret_cast<const float4*>(c->d_f32);
+  p.xn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp : nullptr;
+  p.yn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp + c->W : nullptr;
   p.nc_rays = c->d_nc;
   p.o0 = c->Oc[0];
   p.o1 = c->Oc[1];
@@ -1012,10 +1131,13 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
     idx += 2;
     ++pairs;
   }
+  if (static_cast<int64_t>(n_img) * HW >= (1ll << 31) || 3 * HW >= (1ll << 31))
+    return fail(c, SL_EINVAL, "one view's stack must be < 2 GiB");
   Params p;
   fill_common(c, p, n_views, H, W);
   p.stack = stack;
   p.stack_vs = stack_vs;
+  p.view_bytes = static_cast<int>(static_cast<int64_t>(n_img) * HW);
   p.tex = tex;
   p.tex_vs = tex_vs;
   p.nc = nc;
@@ -1030,12 +1152,14 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   p.xyz = xyz;
   p.bgr = bgr;
   p.view_offsets = view_offsets;
-  p.mode = (maps ? (M_MAPS | M_ROWS) : 0) | (xyz ? M_CLOUD : 0) | (xyz_dtype == SL_XYZ_F64 && xyz ? M_XYZ64 : 0) |
-           (c->d_nc && xyz ? M_NC : 0);
-  const bool vec = (HW % 16 == 0) && aligned16(stack) && (stack_vs % 16 == 0) && (!tex || (aligned16(tex) && tex_vs % 16 == 0)) &&
+  const int nc_bit = (xyz && c->d_nc) ? M_NC : 0;
+  const int decode_mode = (maps ? (M_MAPS | M_ROWS) : 0) | (xyz ? M_CODES : 0) | nc_bit;
+  const int cloud_mode = xyz ? ((xyz_dtype == SL_XYZ_F64 ? M_XYZ64 : 0) | nc_bit) : -1;
+  const bool vec = (W % 16 == 0) && W >= 64 && aligned16(stack) && (stack_vs % 16 == 0) &&
+                   (!tex || (aligned16(tex) && tex_vs % 16 == 0)) &&
                    (!maps || (aligned16(col_out) && aligned16(row_out) && aligned16(mask_out)));
   HIP_TRY(c, hipSetDevice(c->device));
-  return launch(c, p, vec, mask_mode == SL_MASK_ADAPTIVE, static_cast<hipStream_t>(stream));
+  return launch(c, p, vec, mask_mode == SL_MASK_ADAPTIVE, decode_mode, cloud_mode, static_cast<hipStream_t>(stream));
 }
 
 int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, const uint8_t* tex,
@@ -1058,10 +1182,12 @@ int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, 
   p.xyz = xyz;
   p.bgr = bgr;
   p.view_offsets = view_offsets;
-  p.mode = M_FROMMAPS | M_CLOUD | (xyz_dtype == SL_XYZ_F64 ? M_XYZ64 : 0) | (c->d_nc ? M_NC : 0);
-  const bool vec = (HW % 16 == 0) && aligned16(col_map) && aligned16(mask) && aligned16(tex);
+  const int nc_bit = c->d_nc ? M_NC : 0;
+  const int decode_mode = M_FROMMAPS | M_CODES | nc_bit;
+  const int cloud_mode = (xyz_dtype == SL_XYZ_F64 ? M_XYZ64 : 0) | nc_bit;
+  const bool vec = (W % 16 == 0) && W >= 64 && aligned16(col_map) && aligned16(mask) && aligned16(tex);
   HIP_TRY(c, hipSetDevice(c->device));
-  return launch(c, p, vec, false, static_cast<hipStream_t>(stream));
+  return launch(c, p, vec, false, decode_mode, cloud_mode, static_cast<hipStream_t>(stream));
 }
 
 int sl_sync(sl_ctx* c, void* stream) {
@@ -1083,7 +1209,7 @@ int sl_profile_enable(sl_ctx* c, int max_launches) {
   for (hipEvent_t e : c->prof_ev) HIP_TRY(c, hipEventDestroy(e));
   c->prof_ev.clear();
   c->prof_n = 0;
-  for (int i = 0; i < 3 * max_launches; ++i) {
+  for (int i = 0; i < kProfEv * max_launches; ++i) {
     hipEvent_t e;
     HIP_TRY(c, hipEventCreate(&e));
     c->prof_ev.push_back(e);
@@ -1091,21 +1217,22 @@ int sl_profile_enable(sl_ctx* c, int max_launches) {
   return SL_OK;
 }
 
-int sl_profile_read(sl_ctx* c, double* stats_ms, double* decode_ms, int* launches) {
+int sl_profile_read(sl_ctx* c, double* stats_ms, double* decode_ms, double* cloud_ms, int* launches) {
   if (!c) return SL_EINVAL;
   HIP_TRY(c, hipSetDevice(c->device));
-  double a = 0.0, b = 0.0;
+  double t[3] = {0.0, 0.0, 0.0};
   for (int i = 0; i < c->prof_n; ++i) {
-    hipEvent_t* ev = &c->prof_ev[3 * i];
-    HIP_TRY(c, hipEventSynchronize(ev[2]));
-    float t0 = 0.f, t1 = 0.f;
-    HIP_TRY(c, hipEventElapsedTime(&t0, ev[0], ev[1]));
-    HIP_TRY(c, hipEventElapsedTime(&t1, ev[1], ev[2]));
-    a += t0;
-    b += t1;
+    hipEvent_t* ev = &c->prof_ev[kProfEv * i];
+    HIP_TRY(c, hipEventSynchronize(ev[kProfEv - 1]));
+    for (int k = 0; k < 3; ++k) {
+      float ms = 0.f;
+      HIP_TRY(c, hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      t[k] += ms;
+    }
   }
-  if (stats_ms) *stats_ms = a;
-  if (decode_ms) *decode_ms = b;
+  if (stats_ms) *stats_ms = t[0];
+  if (decode_ms) *decode_ms = t[1];
+  if (cloud_ms) *cloud_ms = t[2];
   if (launches) *launches = c->prof_n;
   c->prof_n = 0;
   return SL_OK;
