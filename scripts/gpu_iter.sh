@@ -1,4 +1,4 @@
-# quick iteration: GPU parity tests + kernel bench over build variants
+# quick iteration: GPU parity tests + kernel bench (SLGPU_DEBUG values as args)
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -7,10 +7,8 @@ rc=$?
 tail -3 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 : > gpurun_out/kbench.log
-for lib in "" build/libslgpu_occ3.so build/libslgpu_occ4.so; do
-  [ -n "$lib" ] && [ ! -f "$lib" ] && continue
-  echo "lib=$lib" >> gpurun_out/kbench.log
-  SLGPU_LIB=$lib timeout -k 10 120 python -u scripts/kbench.py "$@" >> gpurun_out/kbench.log 2>&1 || exit $?
+for d in "${@:-0}"; do
+  SLGPU_DEBUG=$d timeout -k 10 120 python -u scripts/kbench.py >> gpurun_out/kbench.log 2>&1 || exit $?
 done
-grep -E "variant|lib=" gpurun_out/kbench.log
+grep -E "variant" gpurun_out/kbench.log | grep -v torch
 exit $rc

@@ -93,7 +93,8 @@ struct Params {
   int mask_mode;
   int mode;
   int dbg;  // measurement-only ablations (SLGPU_DEBUG): 1 = tile from blockIdx, 2 = no look-back,
-            // 4 = no f64 point math, 8 = no f32 point/no-point decision
+            // 4 = no k_cloud work after the ranks, 8 = no point/no-point
+            // decision, 16 = k_cloud stores without point math, 32 = f32 stand-in
   int Wp;
   const double4* planes;
   const float4* planes32;  // f32 copies for the point/no-point pre-decision
@@ -184,19 +185,29 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p, int vec) {
 
   const uint8_t* vb = p.stack + view * p.stack_vs;
   int mx = -1024;
-  for (int64_t c = blockIdx.x; c < p.tiles_per_view; c += gridDim.x) {
-    const int64_t px0 = c * kTile + static_cast<int64_t>(tid) * kPx;
-    const int n = static_cast<int>(min<int64_t>(max<int64_t>(p.HW - px0, 0), kPx));
-    if (n == 0) continue;
-    const uint4 w = ld16(vb + px0, n, vec);
-    const uint4 b = ld16(vb + p.HW + px0, n, vec);
+  // kBatch chunks per iteration: all their loads are issued before any is used
+  constexpr int kBatch = 4;
+  for (int64_t c0 = blockIdx.x; c0 < p.tiles_per_view; c0 += kBatch * gridDim.x) {
+    uint4 w[kBatch], b[kBatch];
+    int n[kBatch];
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      if (k < n) {
-        const int bk = static_cast<int>(byte_of(b, k));
-        const int wk = static_cast<int>(byte_of(w, k));
-        atomicAdd(&sh[wid][bk], 1u);
-        mx = max(mx, wk - bk);
+    for (int i = 0; i < kBatch; ++i) {
+      const int64_t px0 = (c0 + static_cast<int64_t>(i) * gridDim.x) * kTile + static_cast<int64_t>(tid) * kPx;
+      n[i] = static_cast<int>(min<int64_t>(max<int64_t>(p.HW - px0, 0), kPx));
+      const int64_t pl = n[i] > 0 ? px0 : 0;
+      w[i] = ld16(vb + pl, n[i], vec);
+      b[i] = ld16(vb + p.HW + pl, n[i], vec);
+    }
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        if (k < n[i]) {
+          const int bk = static_cast<int>(byte_of(b[i], k));
+          const int wk = static_cast<int>(byte_of(w[i], k));
+          atomicAdd(&sh[wid][bk], 1u);
+          mx = max(mx, wk - bk);
+        }
       }
     }
   }
@@ -307,6 +318,22 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p, int vec) {
 }
 
 // -------------------------------------------------------------- k_decode ----
+
+// Advance pixel coordinates (u, v) by 64 pixels.  On the vector path W >= 64,
+// so at most one row wrap: branch-free selects.  Otherwise loop.
+__device__ __forceinline__ void step64(int& u, int& v, int W, int H, bool vec) {
+  u += 64;
+  if (vec) {
+    const bool wrap = u >= W;
+    u -= wrap ? W : 0;
+    v = min(v + (wrap ? 1 : 0), H - 1);
+  } else {
+    while (u >= W) {
+      u -= W;
+      v = min(v + 1, H - 1);
+    }
+  }
+}
 
 // ------------------------------------------------------------------ layout ----
 // A workgroup (4 waves) owns a tile of kTile = 4096 pixels; wave w owns the
@@ -543,8 +570,34 @@ __global__ __launch_bounds__(kThreads, 2) void k_decode(Params p) {
   __syncthreads();
 
   // ======================= B) interleaved layout =======================
+  // Program order: every gather of the point decision, then the map stores,
+  // then the decisions and record stores -- vmcnt counts loads and stores in
+  // one in-order queue, so no load may wait behind a store.
   const int64_t wpx = lt * kTile + static_cast<int64_t>(wid) * kWavePx + lane;  // step-0 pixel
   const int64_t o = view * HW;
+  const bool codes = (mode & M_CODES) != 0;
+  const int W = p.W;
+  float4 pf[kPx];
+  float xs[kPx], ys[kPx];
+  uint32_t cc[kPx];
+  if (codes) {
+    int v = static_cast<int>(min<int64_t>(wpx, HW - 1) / W);
+    int u = static_cast<int>(min<int64_t>(wpx, HW - 1) - static_cast<int64_t>(v) * W);
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      cc[k] = min(s_code[wid][64 * k + lane] & 0xffffu, static_cast<uint32_t>(p.Wp - 1)) | (u << 16);
+      pf[k] = p.planes32[cc[k] & 0xffffu];
+      if (mode & M_NC) {
+        const int64_t q = min<int64_t>(wpx + 64 * k, HW - 1);
+        xs[k] = static_cast<float>(p.nc_rays[q]);
+        ys[k] = static_cast<float>(p.nc_rays[HW + q]);
+      } else {
+        xs[k] = p.xn32[u];
+        ys[k] = p.yn32[v];
+      }
+      step64(u, v, W, p.H, vload);
+    }
+  }
   if (mode & M_MAPS) {
 #pragma unroll 4
     for (int k = 0; k < kPx; ++k) {
@@ -557,23 +610,44 @@ __global__ __launch_bounds__(kThreads, 2) void k_decode(Params p) {
       }
     }
   }
-  if (!(mode & M_CODES)) return;
-  const int W = p.W;
-  int v = static_cast<int>(min<int64_t>(wpx, HW - 1) / W);
-  int u = static_cast<int>(min<int64_t>(wpx, HW - 1) - static_cast<int64_t>(v) * W);
+  if (!codes) return;
   int total_w = 0;
-#pragma unroll 4
+#pragma unroll
   for (int k = 0; k < kPx; ++k) {
     const int64_t q = wpx + 64 * k;
-    const int c = static_cast<int>(min(s_code[wid][64 * k + lane] & 0xffffu, static_cast<uint32_t>(p.Wp - 1)));
-    const bool pt = s_mask[wid][64 * k + lane] && has_point(p, mode, c, u, v, min<int64_t>(q, HW - 1));
+    const int c = static_cast<int>(cc[k] & 0xffffu);
+    bool pt = false;
+    if (s_mask[wid][64 * k + lane]) {
+      if (p.dbg & 8) {
+        pt = true;
+      } else {
+        // |n.r| > 1e-6 (sl_system.py:642) decided in f32 with a rigorous
+        // error bound B: the f32 rounding of the inputs, of the ray and of the
+        // dot product stay below 2^-21 of S = sum|n_i r_i|, and B uses 2^-18.
+        // Pixels within B of the threshold take the exact f64 arithmetic.
+        const float4 f = pf[k];
+        float zf, inv;
+        if (mode & M_NC) {
+          zf = static_cast<float>(p.nc_rays[2 * HW + min<int64_t>(q, HW - 1)]);
+          inv = 1.0f;
+        } else {
+          zf = 1.0f;
+          inv = __frsqrt_rn(xs[k] * xs[k] + ys[k] * ys[k] + 1.0f);
+        }
+        const float a = fabsf((f.x * xs[k] + f.y * ys[k] + f.z * zf) * inv);
+        const float S = (fabsf(f.x * xs[k]) + fabsf(f.y * ys[k]) + fabsf(f.z * zf)) * inv;
+        const float B = S * 3.814697265625e-06f;  // 2^-18
+        if (a > 1e-6f + B) {
+          pt = true;
+        } else if (a >= 1e-6f - B) {
+          const int u = static_cast<int>(cc[k] >> 16);
+          const int v = static_cast<int>(min<int64_t>(q, HW - 1) / W);
+          pt = has_point(p, mode, c, u, v, min<int64_t>(q, HW - 1));
+        }
+      }
+    }
     total_w += __popcll(__ballot(pt));
     if (q < HW) p.codes[o + q] = static_cast<uint16_t>(c | (pt ? 0x8000 : 0));
-    u += 64;
-    while (u >= W) {
-      u -= W;
-      v = min(v + 1, p.H - 1);
-    }
   }
   if (lane == 0) s_wsum[wid] = total_w;
   __syncthreads();
@@ -624,7 +698,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_cloud(Params p) {
   const int mode = MODE >= 0 ? MODE : p.mode;
   const bool vload = VEC > 0;
 
-  __shared__ uint32_t s_code[kWaves][kWavePx];  // record16
+  __shared__ uint16_t s_code[kWaves][kWavePx];  // record16
   __shared__ uint32_t s_aux[kWaves][kWavePx];   // B | G << 8 | R << 16
   __shared__ int s_wsum[kWaves];
 
@@ -634,6 +708,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_cloud(Params p) {
   const int64_t HW = p.HW;
   const int view = static_cast<int>(blockIdx.x / p.tiles_per_view);
   const int64_t lt = blockIdx.x - static_cast<int64_t>(view) * p.tiles_per_view;
+  const long long tile_base = p.tile_offsets[blockIdx.x];  // issued early, used after the scan
 
   // ============ A) streaming layout: records + colour -> LDS rows ============
   {
@@ -678,19 +753,24 @@ __global__ __launch_bounds__(kThreads, 2) void k_cloud(Params p) {
       tq[1] = make_uint4(t[4], t[5], t[6], t[7]);
       tq[2] = make_uint4(t[8], t[9], t[10], t[11]);
     }
-    uint32_t* lc = &s_code[wid][lane * kPx];
+    uint16_t* lc = &s_code[wid][lane * kPx];
     uint32_t* la = &s_aux[wid][lane * kPx];
+    if (n_px < kPx) {  // tail pixels are not points
+#pragma unroll
+      for (int k = 0; k < kPx; ++k)
+        if (k >= n_px) d[k >> 1] &= ~(0xffffu << (16 * (k & 1)));
+    }
+    *reinterpret_cast<uint4*>(lc) = make_uint4(d[0], d[1], d[2], d[3]);
+    *reinterpret_cast<uint4*>(lc + 8) = make_uint4(d[4], d[5], d[6], d[7]);
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      uint32_t aw[4], cw[4];
+      uint32_t aw[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int k = 4 * w + e, b = 3 * k;
         aw[e] = byte_of(tq[b >> 4], b & 15) | (byte_of(tq[(b + 1) >> 4], (b + 1) & 15) << 8) |
                 (byte_of(tq[(b + 2) >> 4], (b + 2) & 15) << 16);
-        cw[e] = (k < n_px) ? ((d[k >> 1] >> (16 * (k & 1))) & 0xffffu) : 0u;
       }
-      *reinterpret_cast<uint4*>(lc + 4 * w) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
       *reinterpret_cast<uint4*>(la + 4 * w) = make_uint4(aw[0], aw[1], aw[2], aw[3]);
     }
   }
@@ -715,50 +795,82 @@ __global__ __launch_bounds__(kThreads, 2) void k_cloud(Params p) {
   }
   if (lane == 0) s_wsum[wid] = total_w;
   __syncthreads();
-  long long base = p.tile_offsets[blockIdx.x];
+  long long base = tile_base;
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) base += (w < wid) ? s_wsum[w] : 0;
 
   // r = (x, y, 1) / sqrt((x*x + y*y) + 1) (sl_system.py:614-621), plane of the
   // clipped code (:624-633), den = (n0 r0 + n1 r1) + n2 r2 (:638),
   // t = -(n.Oc + d) / den (:639, :643), P = Oc + r t (:648); optional pose.
-  // Four steps at a time are computed branch-free so their chains interleave.
+  // Groups of four steps are computed branch-free so their chains interleave,
+  // and software-pipelined: the operands of group g+1 are loaded before the
+  // points of group g are stored, because vmcnt counts loads and stores in
+  // one in-order queue -- a load issued after a store makes its wait also
+  // wait for that store.
   const int64_t wpx = lt * kTile + static_cast<int64_t>(wid) * kWavePx + lane;
   const int W = p.W;
-  int v = static_cast<int>(min<int64_t>(wpx, HW - 1) / W);
-  int u = static_cast<int>(min<int64_t>(wpx, HW - 1) - static_cast<int64_t>(v) * W);
   const double* pose = p.poses ? p.poses + 16 * view : nullptr;
+  struct Ops {
+    double r0[4], r1[4], r2[4];  // rays (Nc) or x, y, - (pinhole)
+    double4 pl[4];
+  };
+  int u = static_cast<int>(min<int64_t>(wpx, HW - 1) % W);
+  int v = static_cast<int>(min<int64_t>(wpx, HW - 1) / W);
+  auto fetch = [&](int g, Ops& op) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = g + e;
+      if (mode & M_NC) {
+        const int64_t q = min<int64_t>(wpx + 64 * k, HW - 1);
+        op.r0[e] = p.nc_rays[q];
+        op.r1[e] = p.nc_rays[HW + q];
+        op.r2[e] = p.nc_rays[2 * HW + q];
+      } else {
+        op.r0[e] = p.xn[u];
+        op.r1[e] = p.yn[v];
+      }
+      op.pl[e] = p.planes[s_code[wid][64 * k + lane] & 0x7fffu];
+      step64(u, v, W, p.H, vload);
+    }
+  };
+  Ops cur, nxt;
+  fetch(0, cur);
 #pragma unroll
   for (int g = 0; g < kPx; g += 4) {
+    if (g + 4 < kPx) fetch(g + 4, nxt);
     if (((steps >> g) & 0xfu) != 0u && !(p.dbg & 4)) {
       double X[4], Y[4], Z[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int k = g + e;
-        int uu = u, vv = v;
-#pragma unroll
-        for (int s = 0; s < e; ++s) {
-          uu += 64;
-          while (uu >= W) {
-            uu -= W;
-            vv = min(vv + 1, p.H - 1);
-          }
+        if (p.dbg & 16) {  // measurement only: stores without any point math
+          X[e] = cur.r0[e];
+          Y[e] = cur.r1[e];
+          Z[e] = cur.pl[e].w;
+          continue;
+        }
+        if (p.dbg & 32) {  // measurement only: f32 stand-in for the f64 math
+          const float x = static_cast<float>(cur.r0[e]), y = static_cast<float>(cur.r1[e]);
+          const float in = __frsqrt_rn(x * x + y * y + 1.0f);
+          const float4 pf = make_float4(cur.pl[e].x, cur.pl[e].y, cur.pl[e].z, cur.pl[e].w);
+          const float tt = -pf.w / ((pf.x * x + pf.y * y + pf.z) * in);
+          X[e] = x * in * tt;
+          Y[e] = y * in * tt;
+          Z[e] = in * tt;
+          continue;
         }
         double r0, r1, r2;
         if (mode & M_NC) {
-          const int64_t q = min<int64_t>(wpx + 64 * k, HW - 1);
-          r0 = p.nc_rays[q];
-          r1 = p.nc_rays[HW + q];
-          r2 = p.nc_rays[2 * HW + q];
+          r0 = cur.r0[e];
+          r1 = cur.r1[e];
+          r2 = cur.r2[e];
         } else {
-          const double x = p.xn[uu];
-          const double y = p.yn[vv];
+          const double x = cur.r0[e], y = cur.r1[e];
           const double nrm = sqrt((x * x + y * y) + 1.0);
           r0 = x / nrm;
           r1 = y / nrm;
           r2 = 1.0 / nrm;
         }
-        const double4 pl = p.planes[s_code[wid][64 * k + lane] & 0x7fffu];
+        const double4 pl = cur.pl[e];
         const double den = (pl.x * r0 + pl.y * r1) + pl.z * r2;
         const double num = ((pl.x * p.o0 + pl.y * p.o1) + pl.z * p.o2) + pl.w;
         const double t = -num / den;
@@ -797,16 +909,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_cloud(Params p) {
           cc[2] = static_cast<uint8_t>(aux >> 16);
         }
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      u += 64;
-      while (u >= W) {
-        u -= W;
-        v = min(v + 1, p.H - 1);
-      }
-    }
+    cur = nxt;
   }
 }
 
