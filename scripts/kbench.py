@@ -20,6 +20,7 @@ ap.add_argument("--H", type=int, default=2160)
 ap.add_argument("--W", type=int, default=3840)
 ap.add_argument("--views", type=int, default=1)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--only", default=None, help="run one variant")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 rig = synth.Rig(H=a.H, W=a.W)
@@ -46,6 +47,8 @@ print(json.dumps({"variant": "torch_copy", "us": ms * 1e3, "GBps": 2 * st.numel(
 for name, kw in [("maps+cloud", dict(maps=True, cloud=True)), ("cloud", dict(maps=False, cloud=True)),
                  ("maps", dict(maps=True, cloud=False)),
                  ("maps+cloud fixed", dict(maps=True, cloud=True, mask_mode="fixed"))]:
+    if a.only and name != a.only:
+        continue
     out = {}
     for _ in range(3):
         eng.decode_triangulate(st, texture=tx, out=out, **kw)
@@ -53,12 +56,12 @@ for name, kw in [("maps+cloud", dict(maps=True, cloud=True)), ("cloud", dict(map
     eng.profile_enable(a.reps)
     for _ in range(a.reps):
         eng.decode_triangulate(st, texture=tx, out=out, **kw)
-    s_ms, d_ms, c_ms, n = eng.profile_read()
+    d_ms, s_ms, c_ms, n = eng.profile_read()  # decode, count, cloud
     eng.sync()
     npts = int(out["view_offsets"][-1].item()) if "view_offsets" in out else 0
     planes = st.shape[1] if kw.get("maps") else 2 + 2 * 11
     b = px * planes + (3 * px + 15 * npts if kw.get("cloud") else 0) + (9 * px if kw.get("maps") else 0)
     tot = (s_ms + d_ms + c_ms) / n
-    print(json.dumps({"variant": name, "dbg": os.environ.get("SLGPU_DEBUG", "0"), "stats_us": 1e3 * s_ms / n,
+    print(json.dumps({"variant": name, "dbg": os.environ.get("SLGPU_DEBUG", "0"), "count_us": 1e3 * s_ms / n,
                       "decode_us": 1e3 * d_ms / n, "cloud_us": 1e3 * c_ms / n, "total_us": 1e3 * tot,
                       "alg_GBps_total": b / tot / 1e6, "points": npts}))

@@ -234,13 +234,13 @@ class Reconstructor:
         with self._lock:
             _lib.check(self._L.sl_sync(self._ctx, self._stream(stream)), self._ctx, "sl_sync")
 
-    def profile_enable(self, max_launches: int) -> None:
-        """Record HIP events around k_stats / k_decode of the next launches."""
+    def profile_enable(self, max_calls: int) -> None:
+        """Record HIP events around k_decode / k_count / k_cloud of the next calls."""
         with self._lock:
-            _lib.check(self._L.sl_profile_enable(self._ctx, int(max_launches)), self._ctx, "sl_profile_enable")
+            _lib.check(self._L.sl_profile_enable(self._ctx, int(max_calls)), self._ctx, "sl_profile_enable")
 
     def profile_read(self):
-        """-> (k_stats ms, k_decode ms, k_cloud ms, calls) summed since last read."""
+        """-> (k_decode ms, k_count ms, k_cloud ms, calls) summed since last read."""
         a, b, c, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
         with self._lock:
             _lib.check(self._L.sl_profile_read(self._ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),

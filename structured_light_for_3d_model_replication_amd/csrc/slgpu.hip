@@ -8,20 +8,25 @@
 //   triangulation  server/sl_system.py:584-653  (np.where order, clip to Wp-1,
 //                  |n.r| > 1e-6, t = -(n.Oc + d)/(n.r), P = Oc + r t, BGR colour)
 //
-// Kernels (one HIP stream, no host synchronisation between them):
-//   k_stats  : (adaptive mask) 256-bin histogram of the black plane + max(white -
-//              black) per view; the last block of each view turns them into the
-//              float32 np.percentile(black, 95) recipe and integer thresholds.
-//   k_decode : one 4096-pixel tile per workgroup.  Streams the uint8 stack once
-//              with 16-byte buffer loads, forms the Gray bits with a byte-SWAR
-//              compare, Gray->binary in registers, applies the mask, writes the
-//              maps, and decides point/no-point per pixel (f32 with an exact
-//              error bound, f64 when undecided); per-pixel 2-byte records and a
-//              point count per tile.
-//   k_scan   : exclusive scan of the tile counts -> tile and view offsets.
-//   k_cloud  : ray/plane intersection in f64 (reference operation order, no
-//              contraction) for the marked pixels, written at tile offset +
-//              wave-ballot rank: the reference's np.where order, coalesced.
+// Work unit: a CHUNK of 1024 consecutive pixels of one view, owned by one wave.
+// A 256-thread workgroup is 4 chunks of one view; grid = (chunk groups, views).
+//
+// Three kernels on one HIP stream, no host synchronisation between them:
+//   k_decode : streams the uint8 stack once (16-byte loads, lane = 16 contiguous
+//              pixels), forms the Gray bits with a byte-SWAR compare, Gray ->
+//              binary in registers; writes the col/row maps and a 2-byte record
+//              (clipped column code) per pixel.  Adaptive mask: also the 256-bin
+//              histogram of the black plane + max(white - black), per workgroup
+//              in LDS, added to the view's histogram at the end.
+//   k_count  : per wave, the float32 np.percentile(black, 95) thresholds from
+//              the histogram; the mask of every pixel (mask map) and, for the
+//              cloud, the |n.r| > 1e-6 decision (f32 with an exact error bound,
+//              f64 where undecided) as a point bitmask + the chunk's point count
+//              (also added to its 64-chunk super-block sum).
+//   k_cloud  : the chunk's output offset from the super-block and chunk sums,
+//              its points compacted in LDS, the ray/plane intersection in f64
+//              (reference operation order, no contraction), and the stores at
+//              offset + rank -- the reference's np.where order.
 //
 // Everything in this file is compiled with -ffp-contract=off.
 #include <hip/hip_runtime.h>
@@ -44,39 +49,36 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kPx = 16;                  // pixels per lane
-constexpr int kTile = kThreads * kPx;    // pixels per workgroup tile
+constexpr int kPx = 16;                 // pixels per lane in the streaming layout
+constexpr int kChunk = 64 * kPx;        // pixels per wave (one chunk)
 #ifndef SLGPU_RING
-#define SLGPU_RING 16
+#define SLGPU_RING 48
 #endif
-constexpr int kRing = SLGPU_RING;        // pattern planes in flight per lane
+constexpr int kRing = SLGPU_RING;       // stack planes in flight per lane
 
-// k_decode mode bits
-constexpr int M_MAPS = 1;      // k_decode: write col/row/mask maps
-constexpr int M_CODES = 2;     // k_decode: point decision, records + tile counts for k_cloud
-constexpr int M_XYZ64 = 4;     // f64 xyz output (else f32)
-constexpr int M_FROMMAPS = 8;  // k_decode: input is a caller's (col_map, mask) instead of the stack
+// mode bits
+constexpr int M_MAPS = 1;      // k_decode: col/row maps; k_count: mask map
+constexpr int M_CODES = 2;     // k_decode: per-pixel records; k_count: point decision + counts
+constexpr int M_XYZ64 = 4;     // k_cloud: f64 xyz output (else f32)
+constexpr int M_FROMMAPS = 8;  // input is a caller's (col_map, mask) instead of the stack
 constexpr int M_NC = 16;       // rays from a device Nc table instead of pinhole K
-constexpr int M_ROWS = 32;     // decode the row sequence
+constexpr int M_ROWS = 32;     // k_decode: decode the row sequence
+constexpr int M_HIST = 64;     // adaptive mask: k_decode builds the histogram, k_count reads it
 
-constexpr int kStatBlocks = 256;  // k_stats blocks per view (max)
-constexpr int kReps = 16;         // histogram replicas per view
-constexpr int kSlot = 272;        // u32 per replica: 256 bins + max + pad (1088 B)
+constexpr int kSlot = 272;                 // histogram of one view: 256 bins + max + pad (u32)
+constexpr int kHistRep = 32;               // LDS histogram replicas (one per lane of a half-wave)
+constexpr int kHistStride = kHistRep + 1;  // bin stride: replica r of bin b sits in bank (b + r) % 32
+constexpr int kMaxWp = 32768;              // projector columns (record codes are 15 bits)
+constexpr int64_t kMaxChunks = 1 << 14;    // chunks per launch group: bounds k_cloud's prefix reads
 
 struct ViewStats {
-  unsigned done;        // k_stats blocks finished for this view
   int thr_white;        // mask: white > thr_white
   int thr_contrast;     //       white - black > thr_contrast
   float noise_floor;    // np.percentile(black, 95) (float32)
   float dynamic_range;  // max(white - black) (float32)
-  unsigned pad[11];
+  unsigned pad[12];
 };
 static_assert(sizeof(ViewStats) % 64 == 0, "ViewStats keeps 64-B alignment");
-
-struct Header {
-  unsigned error;  // sticky device-side failure (reported by sl_sync as SL_ETIMEOUT)
-  unsigned pad[15];
-};
 
 struct Params {
   const uint8_t* stack;
@@ -88,24 +90,28 @@ struct Params {
   const uint8_t* in_mask;
   int64_t HW;
   int H, W;
-  int n_views, tiles_per_view;
+  int n_views;
+  int cpv;           // chunks per view
+  int64_t n_chunks;  // n_views * cpv
   int nc, nr, kc, kr;  // code bits and available bit planes (pairs)
-  int mask_mode;
   int mode;
-  int dbg;  // measurement-only ablations (SLGPU_DEBUG): 1 = tile from blockIdx, 2 = no look-back,
-            // 4 = no k_cloud work after the ranks, 8 = no point/no-point
-            // decision, 16 = k_cloud stores without point math, 32 = f32 stand-in
+  int dbg;  // measurement-only ablations (SLGPU_DEBUG env): 1 = k_cloud without point math,
+            // 2 = k_cloud without xyz/colour stores, 4 = k_cloud without operand gathers,
+            // 8 = k_cloud stops after its loads + rank scan, 16 = ... after the LDS compaction,
+            // 32 = k_count with the fixed thresholds, 64 = k_count without the |n.r| test,
+            // 128 = k_count without plane gathers, 256 = k_count without super-block atomics
   int Wp;
-  const double4* planes;
-  const float4* planes32;  // f32 copies for the point/no-point pre-decision
-  const double* xn;
-  const double* yn;
+  const double4* planes;   // (n0, n1, n2, num = n.Oc + d) per projector column
+  const float4* planes32;  // f32 (n0, n1, n2, -) for the point/no-point pre-decision
+  const double* xn;        // (u - cx) / fx
+  const double* yn;        // (v - cy) / fy
   const float* xn32;
   const float* yn32;
-  const double* nc_rays;
-  double o0, o1, o2;
+  const double* nc_rays;   // Nc table [3][HW] or null
+  double o0, o1, o2;       // Oc
   const double* poses;
-  uint16_t* codes;  // [view][HW] packed records (ctx scratch)
+  uint16_t* codes;   // [view][HW] records: min(col, Wp-1)
+  uint64_t* ptmask;  // [chunk][16] point bits: bit i of word w = pixel 64 w + i of the chunk
   int32_t* col_out;
   int32_t* row_out;
   uint8_t* mask_out;
@@ -113,10 +119,11 @@ struct Params {
   uint8_t* bgr;
   int64_t* view_offsets;
   ViewStats* stats;
-  unsigned* part;  // k_stats histogram replicas [view][kReps][kSlot]
-  int* tile_counts;          // k_decode -> k_scan
-  long long* tile_offsets;   // k_scan -> k_cloud
-  Header* hdr;
+  unsigned* hist;       // [view][kSlot] accumulated by this launch's k_decode
+  unsigned* hist_zero;  // [view][kSlot] zeroed by this launch's k_decode (the next launch's hist)
+  const int64_t* base_in;  // points of the earlier launch groups of this call, or null
+  int* chunk_counts;       // k_count -> k_cloud: points per chunk
+  int* block_sums;         // k_count -> k_cloud: points per workgroup (4 chunks)
 };
 
 // ---------------------------------------------------------------- helpers ----
@@ -158,566 +165,618 @@ __device__ __forceinline__ uint32_t gray_to_binary(uint32_t g) {
   return g;
 }
 
-// --------------------------------------------------------------- k_stats ----
-// grid (bx <= kStatBlocks, n_views).  Builds, per view, the 256-bin histogram
-// of the black plane and max(white - black):
-//   * per-wave LDS histograms, then no-return device atomics into one of
-//     kReps replicas of the view's histogram (blockIdx % kReps), so no more
-//     than bx/kReps blocks ever add to one address;
-//   * every wave drains its atomics (vmcnt(0)), then one lane adds to the
-//     view's arrival counter; the block whose add is last reads (and zeroes)
-//     the replicas with returning atomics and evaluates numpy's float32
-//     percentile recipe.  The replicas are left zeroed for the next call.
-__global__ __launch_bounds__(kThreads) void k_stats(Params p, int vec) {
-  const int tid = threadIdx.x;
-  const int view = blockIdx.y;
-
-  __shared__ unsigned sh[kWaves][256];
-  __shared__ unsigned cdf[256];
-  __shared__ int s_max[kWaves];
-  __shared__ long long s_k[2];
-  __shared__ int s_v[2];
-  __shared__ float s_gamma;
-  __shared__ int s_last;
-  const int wid = tid >> 6;
-  for (int i = tid; i < kWaves * 256; i += kThreads) (&sh[0][0])[i] = 0u;
-  __syncthreads();
-
-  const uint8_t* vb = p.stack + view * p.stack_vs;
-  int mx = -1024;
-  // kBatch chunks per iteration: all their loads are issued before any is used
-  constexpr int kBatch = 4;
-  for (int64_t c0 = blockIdx.x; c0 < p.tiles_per_view; c0 += kBatch * gridDim.x) {
-    uint4 w[kBatch], b[kBatch];
-    int n[kBatch];
+// Inclusive prefix sum over the 64 lanes of a wave.
+__device__ __forceinline__ int wave_incl_scan(int s, int lane) {
 #pragma unroll
-    for (int i = 0; i < kBatch; ++i) {
-      const int64_t px0 = (c0 + static_cast<int64_t>(i) * gridDim.x) * kTile + static_cast<int64_t>(tid) * kPx;
-      n[i] = static_cast<int>(min<int64_t>(max<int64_t>(p.HW - px0, 0), kPx));
-      const int64_t pl = n[i] > 0 ? px0 : 0;
-      w[i] = ld16(vb + pl, n[i], vec);
-      b[i] = ld16(vb + p.HW + pl, n[i], vec);
-    }
-#pragma unroll
-    for (int i = 0; i < kBatch; ++i) {
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) {
-        if (k < n[i]) {
-          const int bk = static_cast<int>(byte_of(b[i], k));
-          const int wk = static_cast<int>(byte_of(w[i], k));
-          atomicAdd(&sh[wid][bk], 1u);
-          mx = max(mx, wk - bk);
-        }
-      }
-    }
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(s, d, 64);
+    if (lane >= d) s += t;
   }
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
-  if ((tid & 63) == 0) s_max[wid] = mx;
-  __syncthreads();
-  unsigned* rep = p.part + (static_cast<int64_t>(view) * kReps + blockIdx.x % kReps) * kSlot;
-  {
-    const unsigned cnt = sh[0][tid] + sh[1][tid] + sh[2][tid] + sh[3][tid];
-    if (cnt) atomicAdd(rep + tid, cnt);
-  }
-  if (tid == 0) {
-    int m = s_max[0];
-#pragma unroll
-    for (int w = 1; w < kWaves; ++w) m = max(m, s_max[w]);
-    if (m > -1024) atomicMax(rep + 256, static_cast<unsigned>(m + 1024));
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(&p.stats[view].done, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (prev == gridDim.x - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-
-  // ---- last block of this view: read + zero the replicas, thresholds ----
-  unsigned* reps = p.part + static_cast<int64_t>(view) * kReps * kSlot;
-  unsigned h = 0u;
-  {
-    unsigned v[kReps];
-#pragma unroll
-    for (int r = 0; r < kReps; ++r) v[r] = atomicExch(reps + r * kSlot + tid, 0u);
-#pragma unroll
-    for (int r = 0; r < kReps; ++r) h += v[r];
-  }
-  int m = -1024;
-  if (tid < kReps) {
-    const unsigned mv = atomicExch(reps + tid * kSlot + 256, 0u);
-    if (mv) m = static_cast<int>(mv) - 1024;
-  }
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
-  cdf[tid] = h;
-  if ((tid & 63) == 0) s_max[wid] = m;
-  if (tid == 0) __hip_atomic_store(&p.stats[view].done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {  // inclusive scan -> cdf
-    const unsigned t = tid >= d ? cdf[tid - d] : 0u;
-    __syncthreads();
-    cdf[tid] += t;
-    __syncthreads();
-  }
-  if (tid == 0) {
-    // np.percentile(black_f32, 95): q = f32(95)/f32(100); virtual index
-    // (n-1)*q in float32; neighbours floor / floor+1, both clamped to n-1 when
-    // the index is >= n-1 (numpy/lib/_function_base_impl.py _get_indexes);
-    // gamma = index - floor (exact in float32).
-    const long long n = p.HW;
-    const float q = 95.0f / 100.0f;
-    const float fn1 = static_cast<float>(n - 1);
-    const float vi = fn1 * q;
-    long long kp, kn;
-    float gamma;
-    if (vi >= fn1) {
-      kp = kn = n - 1;
-      gamma = 0.0f;
-    } else {
-      const float pf = floorf(vi);
-      kp = static_cast<long long>(pf);
-      kn = static_cast<long long>(pf + 1.0f);
-      gamma = vi - pf;
-    }
-    s_k[0] = kp;
-    s_k[1] = kn;
-    s_gamma = gamma;
-  }
-  __syncthreads();
-  {
-    const unsigned lo = tid ? cdf[tid - 1] : 0u;
-    const unsigned hi = cdf[tid];
-    if (static_cast<long long>(lo) <= s_k[0] && s_k[0] < static_cast<long long>(hi)) s_v[0] = tid;
-    if (static_cast<long long>(lo) <= s_k[1] && s_k[1] < static_cast<long long>(hi)) s_v[1] = tid;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    const float gamma = s_gamma;
-    const float a = static_cast<float>(s_v[0]);
-    const float b = static_cast<float>(s_v[1]);
-    // numpy _lerp: a + (b-a)*t, replaced by b - (b-a)*(1-t) where t >= 0.5
-    const float diff = b - a;
-    float nf = a + diff * gamma;
-    if (gamma >= 0.5f) nf = b - diff * (1.0f - gamma);
-    int mc = s_max[0];
-#pragma unroll
-    for (int w = 1; w < kWaves; ++w) mc = max(mc, s_max[w]);
-    const float dr = static_cast<float>(mc);
-    // white and contrast are integers: x > t  <=>  x > floor(t)
-    const float tw = nf * 1.5f;
-    const float tc = dr * 0.05f;
-    p.stats[view].noise_floor = nf;
-    p.stats[view].dynamic_range = dr;
-    p.stats[view].thr_white = static_cast<int>(floorf(tw));
-    p.stats[view].thr_contrast = static_cast<int>(floorf(tc));
-  }
+  return s;
 }
 
-// -------------------------------------------------------------- k_decode ----
-
-// Advance pixel coordinates (u, v) by 64 pixels.  On the vector path W >= 64,
-// so at most one row wrap: branch-free selects.  Otherwise loop.
-__device__ __forceinline__ void step64(int& u, int& v, int W, int H, bool vec) {
-  u += 64;
-  if (vec) {
-    const bool wrap = u >= W;
-    u -= wrap ? W : 0;
-    v = min(v + (wrap ? 1 : 0), H - 1);
-  } else {
-    while (u >= W) {
-      u -= W;
-      v = min(v + 1, H - 1);
-    }
+__device__ __forceinline__ long long wave_sum64(long long s) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    const unsigned long long u = static_cast<unsigned long long>(s);
+    const unsigned lo = static_cast<unsigned>(__shfl_xor(static_cast<int>(u & 0xffffffffull), d, 64));
+    const unsigned hi = static_cast<unsigned>(__shfl_xor(static_cast<int>(u >> 32), d, 64));
+    s += static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo);
   }
+  return s;
 }
 
-// ------------------------------------------------------------------ layout ----
-// A workgroup (4 waves) owns a tile of kTile = 4096 pixels; wave w owns the
-// tile's pixels [w*1024, (w+1)*1024).
-//   streaming layout  : lane l holds 16 contiguous pixels -> 16-byte loads and
-//                       stores, fully coalesced;
-//   interleaved layout: in step k lane l holds pixel k*64 + l -> coalesced
-//                       table/plane gathers and per-pixel stores.
-// Per-wave LDS rows transpose one layout into the other.
-//
-// Pipeline (one stream): k_stats -> k_decode -> k_scan -> k_cloud.
-//   k_decode : Gray decode + mask + point/no-point decision; per-pixel 2-byte
-//              records and one point count per tile;
-//   k_scan   : exclusive scan of the tile counts (tile and view offsets);
-//   k_cloud  : exact f64 points written at their final, np.where-ordered
-//              positions.  No inter-workgroup waits anywhere.
-constexpr int kWavePx = 64 * kPx;
+__device__ __forceinline__ int wave_sum(int s) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  return s;
+}
 
-// Is |n.r| > 1e-6 (sl_system.py:642) for the pixel at (u, v) / ray index q
-// whose clipped column code is c?  Decided in f32 with a rigorous error bound
-// B: the f32 rounding of the inputs, of the ray and of the dot product stay
-// below 2^-21 of S = sum|n_i r_i|, and B uses 2^-18.  Pixels within B of the
-// threshold are decided by the exact f64 reference arithmetic.
-__device__ __forceinline__ bool has_point(const Params& p, int mode, int c, int u, int v, int64_t q) {
-  const float4 pf = p.planes32[c];
-  float x, y, z, inv;
-  if (mode & M_NC) {
-    x = static_cast<float>(p.nc_rays[q]);
-    y = static_cast<float>(p.nc_rays[p.HW + q]);
-    z = static_cast<float>(p.nc_rays[2 * p.HW + q]);
-    inv = 1.0f;
+// ------------------------------------------------------------ thresholds ----
+// np.percentile(black_f32, 95) and max(white - black) of one view
+// (sl_system.py:526-535) from its 256-bin histogram, evaluated by one wave
+// (lane l holds bins 4l..4l+3): numpy 2.x's float32 recipe -- q = f32(95) /
+// f32(100); virtual index (n-1)*q in float32; neighbours floor / floor+1, both
+// clamped to n-1 when the index is >= n-1 (numpy/lib/_function_base_impl.py
+// _get_indexes); gamma = index - floor; _lerp a + (b-a) g, replaced by
+// b - (b-a)(1-g) where g >= 0.5.  white and contrast are integers, so
+// `x > t` is `x > floor(t)`: the integer thresholds returned.
+struct Thresholds {
+  int white, contrast;
+  float noise_floor, dynamic_range;
+};
+
+__device__ Thresholds thresholds_from_hist(const unsigned* h, int64_t n, int lane) {
+  const uint4 b4 = reinterpret_cast<const uint4*>(h)[lane];
+  const int dmax = static_cast<int>(h[256]) - 1024;
+  const int s4 = static_cast<int>(b4.x + b4.y + b4.z + b4.w);
+  const int incl = wave_incl_scan(s4, lane);
+  const long long e0 = incl - s4;  // pixels below bin 4 lane
+  const float q = 95.0f / 100.0f;
+  const float fn1 = static_cast<float>(n - 1);
+  const float vi = fn1 * q;
+  long long kp, kn;
+  float gamma;
+  if (vi >= fn1) {
+    kp = kn = n - 1;
+    gamma = 0.0f;
   } else {
-    x = p.xn32[u];
-    y = p.yn32[v];
-    z = 1.0f;
-    inv = __frsqrt_rn(x * x + y * y + 1.0f);
+    const float pf = floorf(vi);
+    kp = static_cast<long long>(pf);
+    kn = static_cast<long long>(pf + 1.0f);
+    gamma = vi - pf;
   }
-  const float a = fabsf((pf.x * x + pf.y * y + pf.z * z) * inv);
-  const float S = (fabsf(pf.x * x) + fabsf(pf.y * y) + fabsf(pf.z * z)) * inv;
-  const float B = S * 3.814697265625e-06f;  // 2^-18
-  if (a > 1e-6f + B) return true;
-  if (a < 1e-6f - B) return false;
+  // order statistic k = the bin b with cdf[b-1] <= k < cdf[b]
+  auto value_at = [&](long long k) -> int {
+    const long long c1 = e0 + b4.x, c2 = c1 + b4.y, c3 = c2 + b4.z, c4 = c3 + b4.w;
+    int v = -1;
+    if (e0 <= k && k < c1) v = 4 * lane;
+    else if (c1 <= k && k < c2) v = 4 * lane + 1;
+    else if (c2 <= k && k < c3) v = 4 * lane + 2;
+    else if (c3 <= k && k < c4) v = 4 * lane + 3;
+    const unsigned long long m = __ballot(v >= 0);
+    const int src = m ? static_cast<int>(__ffsll(static_cast<long long>(m))) - 1 : 0;
+    return __shfl(v, src, 64);
+  };
+  const float a = static_cast<float>(value_at(kp));
+  const float b = static_cast<float>(value_at(kn));
+  const float diff = b - a;
+  float nf = a + diff * gamma;
+  if (gamma >= 0.5f) nf = b - diff * (1.0f - gamma);
+  const float dr = static_cast<float>(dmax);
+  Thresholds t;
+  t.noise_floor = nf;
+  t.dynamic_range = dr;
+  t.white = static_cast<int>(floorf(nf * 1.5f));
+  t.contrast = static_cast<int>(floorf(dr * 0.05f));
+  return t;
+}
+
+// ------------------------------------------------------- point decision ----
+
+// Is |n.r| > 1e-6 (sl_system.py:638-642) for the pixel (u, v) / ray index q
+// with clipped column code c, in the reference's exact f64 arithmetic?
+// (Out of line: the rare undecided case.  Plain pointers, so that no copy of
+// the kernel arguments is made.)
+__device__ __noinline__ bool has_point_f64(const double4* planes, const double* xn, const double* yn,
+                                           const double* nc_rays, int64_t HW, int c, int u, int v, int64_t q) {
   double r0, r1, r2;
-  if (mode & M_NC) {
-    r0 = p.nc_rays[q];
-    r1 = p.nc_rays[p.HW + q];
-    r2 = p.nc_rays[2 * p.HW + q];
+  if (nc_rays) {
+    r0 = nc_rays[q];
+    r1 = nc_rays[HW + q];
+    r2 = nc_rays[2 * HW + q];
   } else {
-    const double xd = p.xn[u], yd = p.yn[v];
+    const double xd = xn[u], yd = yn[v];
     const double nrm = sqrt((xd * xd + yd * yd) + 1.0);
     r0 = xd / nrm;
     r1 = yd / nrm;
     r2 = 1.0 / nrm;
   }
-  const double4 pl = p.planes[c];
+  const double4 pl = planes[c];
   return fabs((pl.x * r0 + pl.y * r1) + pl.z * r2) > 1e-6;
 }
 
+// The same decision in f32 with a rigorous error bound B: the f32 rounding of
+// the inputs, of the ray and of the dot product stay below 2^-21 of
+// S = sum|n_i r_i| (B uses 2^-18), plus an absolute 2^-20 * 1e-6 that covers
+// the f32 rounding of the threshold itself.  Pixels within B of the threshold
+// take the exact f64 arithmetic.  (x, y, z) is the unnormalised pinhole ray
+// (z = 1, inv = 1/|r|) or the Nc ray (inv = 1).
+__device__ __forceinline__ bool has_point(const Params& p, int mode, const float4& f, int c, float x, float y,
+                                          float z, float inv, int u, int v, int64_t q) {
+  const float a = fabsf((f.x * x + f.y * y + f.z * z) * inv);
+  const float S = (fabsf(f.x * x) + fabsf(f.y * y) + fabsf(f.z * z)) * inv;
+  const float B = S * 3.814697265625e-06f + 9.5367431640625e-13f;  // 2^-18 S + 2^-20 * 1e-6
+  if (a > 1e-6f + B) return true;
+  if (a < 1e-6f - B) return false;
+  return has_point_f64(p.planes, p.xn, p.yn, (mode & M_NC) ? p.nc_rays : nullptr, p.HW, c, u, v, q);
+}
+
 // ================================================================ k_decode ====
-// gray_decode (sl_system.py:519-577): mask, column and row code of every
-// pixel, streaming the uint8 stack once (M_FROMMAPS: a caller's col_map + mask
-// instead).  Outputs by mode bit:
-//   M_MAPS  col/row int32 + mask u8 maps, full frame (what gray_decode returns);
-//   M_CODES record16 = min(col, Wp-1) | point << 15 per pixel (np.clip,
-//           sl_system.py:626; point = mask & |n.r| > 1e-6) and the tile's
-//           point count, for k_scan / k_cloud.
+// gray_decode (sl_system.py:519-577) for one chunk per wave, in the streaming
+// layout (lane l owns the chunk's pixels [16 l, 16 l + 16)): column and row
+// code of every pixel, reading each plane of the uint8 stack once (M_FROMMAPS:
+// a caller's col_map instead).  Outputs by mode bit:
+//   M_MAPS   col/row int32 maps, full frame, unmasked (what gray_decode
+//            returns), 16-byte stores;
+//   M_CODES  record16 = min(col, Wp-1) (np.clip, sl_system.py:626) per pixel,
+//            for k_count / k_cloud;
+//   M_HIST   the view's black-plane histogram and max(white - black)
+//            (sl_system.py:526-528): LDS replicas bank-skewed so that the
+//            lanes of a half-wave that hit the same bin use 32 different
+//            banks, added to the view's global histogram once per workgroup.
+// Grid (chunk groups, views); waves past the view's last chunk run empty (the
+// workgroup barriers count them).
 template <int KC, int KR, int MODE, int VEC>
-__global__ __launch_bounds__(kThreads, 2) void k_decode(Params p) {
-  constexpr bool kStatic = KC >= 0;
+__global__ __launch_bounds__(kThreads) void k_decode(Params p) {
   const int mode = MODE >= 0 ? MODE : p.mode;
   const int kc = KC >= 0 ? KC : p.kc;
-  const int kr = KR >= 0 ? KR : p.kr;
+  const int krr = (mode & M_ROWS) ? (KR >= 0 ? KR : p.kr) : 0;
   const int nc = p.nc, nr = p.nr;
-  const bool vload = VEC > 0;
+  const bool vec = VEC > 0;
+  const bool hist = (mode & M_HIST) != 0;
 
-  __shared__ uint32_t s_code[kWaves][kWavePx];  // col | row << 16
-  __shared__ uint8_t s_mask[kWaves][kWavePx];
-  __shared__ int s_wsum[kWaves];
-
+  __shared__ unsigned s_hist[256 * kHistStride];
+  __shared__ int s_max[kWaves];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
+  const int view = blockIdx.y;
+  const int civ = blockIdx.x * kWaves + wid;  // chunk in view
+  const bool live = civ < p.cpv;
   const int64_t HW = p.HW;
-  const int view = static_cast<int>(blockIdx.x / p.tiles_per_view);
-  const int64_t lt = blockIdx.x - static_cast<int64_t>(view) * p.tiles_per_view;
+  const int64_t px0 = static_cast<int64_t>(civ) * kChunk + lane * kPx;
+  const int n_px = live ? static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx)) : 0;
+  const int64_t pxl = n_px > 0 ? px0 : 0;  // keep loads unconditional and in bounds
+  const int64_t o = view * HW + px0;
 
-  // ======================= A) streaming layout =======================
-  {
-    const int64_t px0 = lt * kTile + static_cast<int64_t>(tid) * kPx;
-    const int n_px = static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx));
-    const int64_t px_ld = n_px > 0 ? px0 : 0;  // keep loads unconditional and in bounds
-    uint32_t* lc = &s_code[wid][lane * kPx];
-    uint8_t* lm = &s_mask[wid][lane * kPx];
-    if (mode & M_FROMMAPS) {
-      // reconstruct_point_cloud's inputs: col_map (clipped, sl_system.py:626) and mask
-      const int64_t o = view * HW + px_ld;
-      uint32_t col[kPx];
-      uint32_t mw[4] = {0u, 0u, 0u, 0u};
-      if (vload) {
-        const int4* cm = reinterpret_cast<const int4*>(p.in_col + o);
+  // the next launch's histogram (scratch of this one)
+  if (hist && blockIdx.x == 0)
+    for (int i = tid; i < kSlot; i += kThreads) p.hist_zero[view * kSlot + i] = 0u;
+  if (hist) {
+    for (int i = tid; i < 256 * kHistStride; i += kThreads) s_hist[i] = 0u;
+    __syncthreads();
+  }
+
+  uint32_t col[kPx];
+  if (mode & M_FROMMAPS) {
+    // reconstruct_point_cloud's input col_map (clipped below, sl_system.py:626)
+    const int64_t ol = view * HW + pxl;
+    if (vec) {
+      const int4* cm = reinterpret_cast<const int4*>(p.in_col + ol);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int4 v = cm[i];
-          col[4 * i] = v.x;
-          col[4 * i + 1] = v.y;
-          col[4 * i + 2] = v.z;
-          col[4 * i + 3] = v.w;
+      for (int i = 0; i < 4; ++i) {
+        const int4 v = cm[i];
+        col[4 * i] = static_cast<uint32_t>(max(v.x, 0));
+        col[4 * i + 1] = static_cast<uint32_t>(max(v.y, 0));
+        col[4 * i + 2] = static_cast<uint32_t>(max(v.z, 0));
+        col[4 * i + 3] = static_cast<uint32_t>(max(v.w, 0));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) col[k] = k < n_px ? static_cast<uint32_t>(max(p.in_col[ol + k], 0)) : 0u;
+    }
+  } else {
+    // Plane loads: on the vector path a buffer descriptor of the view's stack
+    // (SGPRs) + the lane's 32-bit pixel offset + the plane offset in an SGPR.
+    const uint8_t* vbase = p.stack + view * p.stack_vs;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vbase), 0, p.view_bytes, 0x00020000);
+    const int voff = static_cast<int>(pxl);
+    auto ldp = [&](int plane) -> uint4 {
+      if (vec) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, plane * static_cast<int>(HW), 0);
+        return make_uint4(v[0], v[1], v[2], v[3]);
+      }
+      return ld16(vbase + pxl + static_cast<int64_t>(plane) * HW, n_px, false);
+    };
+    const uint4 wq = ldp(0);
+    const uint4 bq = ldp(1);
+    // ---- Gray bit planes: (pattern, inverse) pairs, columns then rows ----
+    const int npl = 2 * (kc + krr);
+    uint32_t cA[4] = {0, 0, 0, 0}, cB[4] = {0, 0, 0, 0};
+    uint32_t rA[4] = {0, 0, 0, 0}, rB[4] = {0, 0, 0, 0};
+    // Fold one (pattern, inverse) pair into per-byte-lane accumulators:
+    // acc = (acc << 1) | bit holds at most 8 bits per byte lane, so no carry
+    // crosses into the neighbouring pixel; codes of up to 16 bits use A then B.
+    auto consume = [&](const uint4& P, const uint4& I, int pair) {
+      uint32_t m[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) m[w] = gt_msb(word(P, w), word(I, w)) >> 7;
+      if (pair < kc) {
+        if (pair < 8) {
+#pragma unroll
+          for (int w = 0; w < 4; ++w) cA[w] = (cA[w] << 1) | m[w];
+        } else {
+#pragma unroll
+          for (int w = 0; w < 4; ++w) cB[w] = (cB[w] << 1) | m[w];
         }
-        const uint4 mq = *reinterpret_cast<const uint4*>(p.in_mask + o);
+      } else if (pair - kc < 8) {
 #pragma unroll
-        for (int k = 0; k < kPx; ++k) mw[k >> 2] |= (byte_of(mq, k) != 0u && k < n_px) ? (1u << (8 * (k & 3))) : 0u;
+        for (int w = 0; w < 4; ++w) rA[w] = (rA[w] << 1) | m[w];
+      } else {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) rB[w] = (rB[w] << 1) | m[w];
+      }
+    };
+    if (KC >= 0) {
+      // static plane count: unrolled, kRing planes in flight
+      constexpr int NPL = 2 * (KC + (KR > 0 ? KR : 0));
+      constexpr int R = kRing < NPL ? kRing : NPL;
+      uint4 ring[R > 0 ? R : 1];
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (j < npl) ring[j] = ldp(2 + j);
+#pragma unroll
+      for (int pl = 0; pl < NPL; pl += 2) {
+        if (pl < npl) {
+          const uint4 P = ring[pl % R];
+          const uint4 I = ring[(pl + 1) % R];
+          if (pl + R < npl) {
+            ring[pl % R] = ldp(2 + pl + R);
+            ring[(pl + 1) % R] = ldp(3 + pl + R);
+          }
+          consume(P, I, pl >> 1);
+        }
+      }
+    } else {
+      constexpr int R = 16;
+      uint4 ring[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if (j < npl) ring[j] = ldp(2 + j);
+      for (int base = 0; base < npl; base += R) {
+#pragma unroll
+        for (int j = 0; j < R; j += 2) {
+          const int pl = base + j;
+          if (pl < npl) {
+            const uint4 P = ring[j];
+            const uint4 I = ring[j + 1];
+            if (pl + R < npl) {
+              ring[j] = ldp(2 + pl + R);
+              ring[j + 1] = ldp(3 + pl + R);
+            }
+            consume(P, I, pl >> 1);
+          }
+        }
+      }
+    }
+    // ---- Gray -> binary ----
+    const int cBn = kc > 8 ? kc - 8 : 0;
+    const int rBn = krr > 8 ? krr - 8 : 0;
+    const int cSh = nc - kc;
+    const int rSh = nr - krr;
+    uint32_t row[kPx];
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      const int w = k >> 2, sft = 8 * (k & 3);
+      const uint32_t gc = (((cA[w] >> sft) & 0xffu) << cBn) | ((cB[w] >> sft) & 0xffu);
+      const uint32_t gr = (((rA[w] >> sft) & 0xffu) << rBn) | ((rB[w] >> sft) & 0xffu);
+      col[k] = gray_to_binary(gc << cSh);
+      row[k] = (mode & M_ROWS) ? gray_to_binary(gr << rSh) : 0u;
+    }
+    if (mode & M_MAPS) {
+      if (vec) {
+        if (n_px == kPx) {
+          int4* co = reinterpret_cast<int4*>(p.col_out + o);
+          int4* ro = reinterpret_cast<int4*>(p.row_out + o);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            co[i] = make_int4(col[4 * i], col[4 * i + 1], col[4 * i + 2], col[4 * i + 3]);
+            ro[i] = make_int4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
+          }
+        }
       } else {
 #pragma unroll
         for (int k = 0; k < kPx; ++k) {
-          col[k] = k < n_px ? static_cast<uint32_t>(p.in_col[o + k]) : 0u;
-          mw[k >> 2] |= (k < n_px && p.in_mask[o + k] != 0) ? (1u << (8 * (k & 3))) : 0u;
+          if (k < n_px) {
+            p.col_out[o + k] = static_cast<int32_t>(col[k]);
+            p.row_out[o + k] = static_cast<int32_t>(row[k]);
+          }
+        }
+      }
+    }
+    if (hist) {
+      unsigned* hrow = s_hist + (lane & (kHistRep - 1));
+      int mx = -1024;
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        if (k < n_px) {
+          const int bk = static_cast<int>(byte_of(bq, k));
+          atomicAdd(hrow + bk * kHistStride, 1u);
+          mx = max(mx, static_cast<int>(byte_of(wq, k)) - bk);
         }
       }
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        uint32_t cw[4];
+      for (int d = 32; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
+      if (lane == 0) s_max[wid] = mx;
+    }
+  }
+
+  if (mode & M_CODES) {
+    // records for k_count / k_cloud: clipped column code
+    uint32_t rec[kPx / 2];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          cw[e] = static_cast<uint32_t>(min(max(static_cast<int>(col[4 * w + e]), 0), p.Wp - 1));
-        *reinterpret_cast<uint4*>(lc + 4 * w) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-        *reinterpret_cast<uint32_t*>(lm + 4 * w) = mw[w];
+    for (int i = 0; i < kPx / 2; ++i)
+      rec[i] = min(col[2 * i], static_cast<uint32_t>(p.Wp - 1)) |
+               (min(col[2 * i + 1], static_cast<uint32_t>(p.Wp - 1)) << 16);
+    if (vec) {
+      if (n_px == kPx) {
+        uint4* ro = reinterpret_cast<uint4*>(p.codes + o);
+        ro[0] = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+        ro[1] = make_uint4(rec[4], rec[5], rec[6], rec[7]);
       }
     } else {
-      // Plane loads: on the vector path a buffer descriptor of the view's
-      // stack (SGPRs) + the lane's 32-bit pixel offset + the plane offset in an SGPR.
-      const uint8_t* vbase = p.stack + view * p.stack_vs;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vbase), 0, p.view_bytes, 0x00020000);
-      const int voff = static_cast<int>(px_ld);
-      auto ldp = [&](int plane) -> uint4 {
-        if (vload) {
-          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, plane * static_cast<int>(HW), 0);
-          return make_uint4(v[0], v[1], v[2], v[3]);
-        }
-        return ld16(vbase + px_ld + static_cast<int64_t>(plane) * HW, n_px, false);
-      };
-      const uint4 wq = ldp(0);
-      const uint4 bq = ldp(1);
-      // ---- Gray bit planes: (pattern, inverse) pairs, columns then rows ----
-      const int krr = (mode & M_ROWS) ? kr : 0;
-      const int npl = 2 * (kc + krr);
-      uint32_t cA[4] = {0, 0, 0, 0}, cB[4] = {0, 0, 0, 0};
-      uint32_t rA[4] = {0, 0, 0, 0}, rB[4] = {0, 0, 0, 0};
-      // Fold one (pattern, inverse) pair into per-byte-lane accumulators:
-      // acc = (acc << 1) | bit holds at most 8 bits per byte lane, so no carry
-      // crosses into the neighbouring pixel; codes of up to 16 bits use A then B.
-      auto consume = [&](const uint4& P, const uint4& I, int pair) {
-        uint32_t m[4];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) m[w] = gt_msb(word(P, w), word(I, w)) >> 7;
-        if (pair < kc) {
-          if (pair < 8) {
-#pragma unroll
-            for (int w = 0; w < 4; ++w) cA[w] = (cA[w] << 1) | m[w];
-          } else {
-#pragma unroll
-            for (int w = 0; w < 4; ++w) cB[w] = (cB[w] << 1) | m[w];
-          }
-        } else if (pair - kc < 8) {
-#pragma unroll
-          for (int w = 0; w < 4; ++w) rA[w] = (rA[w] << 1) | m[w];
-        } else {
-#pragma unroll
-          for (int w = 0; w < 4; ++w) rB[w] = (rB[w] << 1) | m[w];
-        }
-      };
-      if (kStatic) {
-        // fully unrolled: every plane load issues up front (the widest
-        // memory-level parallelism a wave can have)
-#pragma unroll
-        for (int pr = 0; pr < KC + KR; ++pr)
-          if (pr < kc + krr) consume(ldp(2 + 2 * pr), ldp(3 + 2 * pr), pr);
-      } else {
-        uint4 ring[kRing];
-#pragma unroll
-        for (int j = 0; j < kRing; ++j)
-          if (j < npl) ring[j] = ldp(2 + j);
-        for (int base = 0; base < npl; base += kRing) {
-#pragma unroll
-          for (int j = 0; j < kRing; j += 2) {
-            const int pl = base + j;
-            if (pl < npl) {
-              const uint4 P = ring[j];
-              const uint4 I = ring[j + 1];
-              if (pl + kRing < npl) {
-                ring[j] = ldp(2 + pl + kRing);
-                ring[j + 1] = ldp(3 + pl + kRing);
-              }
-              consume(P, I, pl >> 1);
-            }
-          }
-        }
-      }
-      // ---- mask + Gray -> binary ----
-      int thr_w, thr_c;
-      if (p.mask_mode == SL_MASK_FIXED) {
-        thr_w = 40;
-        thr_c = 10;
-      } else {
-        thr_w = p.stats[view].thr_white;
-        thr_c = p.stats[view].thr_contrast;
-      }
-      const int cBn = kc > 8 ? kc - 8 : 0;
-      const int rBn = krr > 8 ? krr - 8 : 0;
-      const int cSh = nc - kc;
-      const int rSh = nr - krr;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        uint32_t cw[4];
-        uint32_t mw = 0u;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int k = 4 * w + e, sft = 8 * e;
-          const uint32_t gc = (((cA[w] >> sft) & 0xffu) << cBn) | ((cB[w] >> sft) & 0xffu);
-          const uint32_t gr = (((rA[w] >> sft) & 0xffu) << rBn) | ((rB[w] >> sft) & 0xffu);
-          const uint32_t col = gray_to_binary(gc << cSh);
-          const uint32_t row = (mode & M_ROWS) ? gray_to_binary(gr << rSh) : 0u;
-          const int wv = static_cast<int>(byte_of(wq, k));
-          const int bv = static_cast<int>(byte_of(bq, k));
-          const uint32_t ok = ((k < n_px) && (wv > thr_w) && (wv - bv > thr_c)) ? 1u : 0u;
-          cw[e] = col | (row << 16);
-          mw |= ok << sft;
-        }
-        *reinterpret_cast<uint4*>(lc + 4 * w) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
-        *reinterpret_cast<uint32_t*>(lm + 4 * w) = mw;
-      }
+      for (int k = 0; k < kPx; ++k)
+        if (k < n_px) p.codes[o + k] = static_cast<uint16_t>(rec[k >> 1] >> (16 * (k & 1)));
     }
   }
-  __syncthreads();
 
-  // ======================= B) interleaved layout =======================
-  // Program order: every gather of the point decision, then the map stores,
-  // then the decisions and record stores -- vmcnt counts loads and stores in
-  // one in-order queue, so no load may wait behind a store.
-  const int64_t wpx = lt * kTile + static_cast<int64_t>(wid) * kWavePx + lane;  // step-0 pixel
-  const int64_t o = view * HW;
-  const bool codes = (mode & M_CODES) != 0;
-  const int W = p.W;
-  float4 pf[kPx];
-  float xs[kPx], ys[kPx];
-  uint32_t cc[kPx];
-  if (codes) {
-    int v = static_cast<int>(min<int64_t>(wpx, HW - 1) / W);
-    int u = static_cast<int>(min<int64_t>(wpx, HW - 1) - static_cast<int64_t>(v) * W);
+  if (hist) {
+    __syncthreads();
+    unsigned* gh = p.hist + view * kSlot;
+    unsigned cnt = 0u;
+    const unsigned* row = s_hist + tid * kHistStride;
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      cc[k] = min(s_code[wid][64 * k + lane] & 0xffffu, static_cast<uint32_t>(p.Wp - 1)) | (u << 16);
-      pf[k] = p.planes32[cc[k] & 0xffffu];
-      if (mode & M_NC) {
-        const int64_t q = min<int64_t>(wpx + 64 * k, HW - 1);
-        xs[k] = static_cast<float>(p.nc_rays[q]);
-        ys[k] = static_cast<float>(p.nc_rays[HW + q]);
-      } else {
-        xs[k] = p.xn32[u];
-        ys[k] = p.yn32[v];
-      }
-      step64(u, v, W, p.H, vload);
-    }
-  }
-  if (mode & M_MAPS) {
-#pragma unroll 4
-    for (int k = 0; k < kPx; ++k) {
-      const int64_t q = wpx + 64 * k;
-      if (q < HW) {
-        const uint32_t cw = s_code[wid][64 * k + lane];
-        p.col_out[o + q] = static_cast<int32_t>(cw & 0xffffu);
-        p.row_out[o + q] = static_cast<int32_t>(cw >> 16);
-        p.mask_out[o + q] = s_mask[wid][64 * k + lane];
-      }
-    }
-  }
-  if (!codes) return;
-  int total_w = 0;
+    for (int r = 0; r < kHistRep; ++r) cnt += row[r];
+    if (cnt) atomicAdd(gh + tid, cnt);
+    if (tid == 0) {
+      int m = s_max[0];
 #pragma unroll
-  for (int k = 0; k < kPx; ++k) {
-    const int64_t q = wpx + 64 * k;
-    const int c = static_cast<int>(cc[k] & 0xffffu);
-    bool pt = false;
-    if (s_mask[wid][64 * k + lane]) {
-      if (p.dbg & 8) {
-        pt = true;
-      } else {
-        // |n.r| > 1e-6 (sl_system.py:642) decided in f32 with a rigorous
-        // error bound B: the f32 rounding of the inputs, of the ray and of the
-        // dot product stay below 2^-21 of S = sum|n_i r_i|, and B uses 2^-18.
-        // Pixels within B of the threshold take the exact f64 arithmetic.
-        const float4 f = pf[k];
-        float zf, inv;
-        if (mode & M_NC) {
-          zf = static_cast<float>(p.nc_rays[2 * HW + min<int64_t>(q, HW - 1)]);
-          inv = 1.0f;
-        } else {
-          zf = 1.0f;
-          inv = __frsqrt_rn(xs[k] * xs[k] + ys[k] * ys[k] + 1.0f);
-        }
-        const float a = fabsf((f.x * xs[k] + f.y * ys[k] + f.z * zf) * inv);
-        const float S = (fabsf(f.x * xs[k]) + fabsf(f.y * ys[k]) + fabsf(f.z * zf)) * inv;
-        const float B = S * 3.814697265625e-06f;  // 2^-18
-        if (a > 1e-6f + B) {
-          pt = true;
-        } else if (a >= 1e-6f - B) {
-          const int u = static_cast<int>(cc[k] >> 16);
-          const int v = static_cast<int>(min<int64_t>(q, HW - 1) / W);
-          pt = has_point(p, mode, c, u, v, min<int64_t>(q, HW - 1));
-        }
-      }
+      for (int w = 1; w < kWaves; ++w) m = max(m, s_max[w]);
+      if (m > -1024) atomicMax(gh + 256, static_cast<unsigned>(m + 1024));
     }
-    total_w += __popcll(__ballot(pt));
-    if (q < HW) p.codes[o + q] = static_cast<uint16_t>(c | (pt ? 0x8000 : 0));
-  }
-  if (lane == 0) s_wsum[wid] = total_w;
-  __syncthreads();
-  if (tid == 0) {
-    int t = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) t += s_wsum[w];
-    p.tile_counts[blockIdx.x] = t;
   }
 }
 
-// ================================================================== k_scan ====
-// Exclusive scan of the per-tile point counts (tiles of all views in order):
-// tile_offsets[t] = points before tile t; view_offsets[v] = points before view
-// v, view_offsets[V] = total.  One workgroup of 1024 threads.
-__global__ __launch_bounds__(1024) void k_scan(Params p) {
-  __shared__ long long s_part[1024];
-  const int tid = threadIdx.x;
-  const int64_t n = static_cast<int64_t>(p.n_views) * p.tiles_per_view;
-  const int64_t per = (n + 1023) / 1024;
-  const int64_t lo = min<int64_t>(tid * per, n), hi = min<int64_t>(lo + per, n);
-  long long s = 0;
-  for (int64_t i = lo; i < hi; ++i) s += p.tile_counts[i];
-  s_part[tid] = s;
+// ================================================================= k_count ====
+// Per wave (one chunk): the mask thresholds (adaptive: from the view's
+// histogram; fixed: white > 40, contrast > 10), the mask of every pixel
+// (M_MAPS: the mask map) and, for the cloud (M_CODES), the decision
+// |n.r| > 1e-6 (sl_system.py:638-642) of every masked pixel -- f32 with an
+// exact error bound, f64 where undecided -- as point bits, the chunk's point
+// count and its super-block sum.
+// Quad layout: in step s (0..3) lane l holds the 4 pixels 256 s + 4 l + e of
+// the chunk: 4-byte white/black loads and mask stores, 8-byte record loads,
+// and plane gathers of nearby columns.  Every load is issued before any is
+// used (clamped, unconditional addresses).
+template <int VEC>
+__device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view, int civ, int thr_w, int thr_c,
+                                           int lane) {
+  const int mode = p.mode;
+  const bool vec = VEC > 0;
+  const int64_t HW = p.HW;
+  const int64_t cpx = static_cast<int64_t>(civ) * kChunk;
+  const int W = p.W;
+  const bool codes = (mode & M_CODES) != 0;
+  const bool nc = (mode & M_NC) != 0;
+
+  // ---- loads ----
+  uint32_t wv[4], bv[4];  // 4 pixels per step, one byte each
+  uint32_t rc[4][2];      // records: 4 x u16 per step
+  const int64_t px_hi = vec ? HW - 4 : HW - 1;  // clamp for tail loads (keeps 4-pixel alignment)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int64_t px = min<int64_t>(cpx + 256 * s + 4 * lane, px_hi);
+    if (mode & M_FROMMAPS) {
+      wv[s] = bv[s] = 0u;
+    } else if (vec) {
+      const uint8_t* sp = p.stack + view * p.stack_vs + px;
+      wv[s] = *reinterpret_cast<const uint32_t*>(sp);
+      bv[s] = *reinterpret_cast<const uint32_t*>(sp + HW);
+    } else {
+      const uint8_t* sp = p.stack + view * p.stack_vs;
+      uint32_t a = 0u, b = 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t q = min<int64_t>(px + e, HW - 1);
+        a |= static_cast<uint32_t>(sp[q]) << (8 * e);
+        b |= static_cast<uint32_t>(sp[HW + q]) << (8 * e);
+      }
+      wv[s] = a;
+      bv[s] = b;
+    }
+    if (codes) {
+      if (vec) {
+        const uint2 r = *reinterpret_cast<const uint2*>(p.codes + view * HW + px);
+        rc[s][0] = r.x;
+        rc[s][1] = r.y;
+      } else {
+        const uint16_t* rp = p.codes + view * HW;
+        rc[s][0] = rp[min<int64_t>(px, HW - 1)] | (static_cast<uint32_t>(rp[min<int64_t>(px + 1, HW - 1)]) << 16);
+        rc[s][1] = rp[min<int64_t>(px + 2, HW - 1)] | (static_cast<uint32_t>(rp[min<int64_t>(px + 3, HW - 1)]) << 16);
+      }
+    }
+  }
+  uint32_t mk[4] = {0u, 0u, 0u, 0u};  // FROMMAPS: the caller's mask bytes
+  if (mode & M_FROMMAPS) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int64_t px = cpx + 256 * s + 4 * lane;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        mk[s] |= (px + e < HW && p.in_mask[view * HW + px + e] != 0) ? (1u << e) : 0u;
+    }
+  }
+
+  // ---- mask ----
+  uint32_t ok[4];  // bit e: pixel 256 s + 4 lane + e is valid
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int64_t px = cpx + 256 * s + 4 * lane;
+    uint32_t m = 0u;
+    if (mode & M_FROMMAPS) {
+      m = mk[s];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int w = static_cast<int>((wv[s] >> (8 * e)) & 0xffu);
+        const int b = static_cast<int>((bv[s] >> (8 * e)) & 0xffu);
+        m |= (px + e < HW && w > thr_w && w - b > thr_c) ? (1u << e) : 0u;
+      }
+    }
+    ok[s] = m;
+    if (mode & M_MAPS) {
+      const uint32_t bytes = (m & 1u) | ((m & 2u) << 7) | ((m & 4u) << 14) | ((m & 8u) << 21);
+      if (vec) {
+        if (px < HW) *reinterpret_cast<uint32_t*>(p.mask_out + view * HW + px) = bytes;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (px + e < HW) p.mask_out[view * HW + px + e] = static_cast<uint8_t>((m >> e) & 1u);
+      }
+    }
+  }
+  if (!codes) return 0;
+
+  // ---- |n.r| > 1e-6 for the masked pixels ----
+  float4 pf[4][4];
+  float xs[4][4], ys[4];
+  int us[4], vs[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int64_t px = min<int64_t>(cpx + 256 * s + 4 * lane, px_hi);
+    us[s] = static_cast<int>(px % W);
+    vs[s] = static_cast<int>(px / W);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      pf[s][e] = (p.dbg & 128) ? make_float4(0.5f, 0.1f, 0.8f, 0.f)
+                               : p.planes32[(rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu];
+    if (!nc) {
+      if (vec) {
+        const float4 x4 = *reinterpret_cast<const float4*>(p.xn32 + us[s]);
+        xs[s][0] = x4.x;
+        xs[s][1] = x4.y;
+        xs[s][2] = x4.z;
+        xs[s][3] = x4.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xs[s][e] = p.xn32[(us[s] + e) % W];
+      }
+      ys[s] = p.yn32[vs[s]];
+    }
+  }
+  int total = 0;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint32_t nib = 0u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (((ok[s] >> e) & 1u) && (p.dbg & 64)) {
+        nib |= 1u << e;
+      } else if ((ok[s] >> e) & 1u) {
+        const int c = static_cast<int>((rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu);
+        int u = us[s] + e, v = vs[s];
+        if (!vec && u >= W) {
+          u -= W;
+          ++v;
+        }
+        const int64_t q = cpx + 256 * s + 4 * lane + e;
+        float x, y, z, inv;
+        if (nc) {
+          x = static_cast<float>(p.nc_rays[q]);
+          y = static_cast<float>(p.nc_rays[HW + q]);
+          z = static_cast<float>(p.nc_rays[2 * HW + q]);
+          inv = 1.0f;
+        } else {
+          x = xs[s][e];
+          y = vec ? ys[s] : p.yn32[v];
+          z = 1.0f;
+          inv = __frsqrt_rn(x * x + y * y + 1.0f);
+        }
+        if (has_point(p, mode, pf[s][e], c, x, y, z, inv, u, v, q)) nib |= 1u << e;
+      }
+    }
+    total += __popc(nib);
+    // point words of step s: word 4 s + m = the nibbles of lanes 16 m .. 16 m + 15
+    uint32_t lo = (lane & 15) < 8 ? nib << (4 * (lane & 7)) : 0u;
+    uint32_t hi = (lane & 15) >= 8 ? nib << (4 * (lane & 7)) : 0u;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      lo |= __shfl_xor(lo, d, 64);
+      hi |= __shfl_xor(hi, d, 64);
+    }
+    if ((lane & 15) == 0)
+      p.ptmask[gc * kPx + 4 * s + (lane >> 4)] = static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
+  }
+  total = wave_sum(total);
+  if (lane == 0) p.chunk_counts[gc] = total;
+  return total;
+}
+
+// k_count: one chunk per wave, grid (chunk groups of 4, views); the
+// workgroup's point total goes to block_sums for k_cloud's offsets.
+template <int VEC>
+__global__ __launch_bounds__(kThreads) void k_count(Params p) {
+  __shared__ int s_sum[kWaves];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int view = blockIdx.y;
+  const int civ = blockIdx.x * kWaves + wid;
+  const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
+  int thr_w = 40, thr_c = 10;  // fixed: multi_point_cloud_process.py:36-38
+  if ((p.mode & M_HIST) && !(p.dbg & 32)) {
+    const Thresholds t = thresholds_from_hist(p.hist + view * kSlot, p.HW, lane);
+    thr_w = t.white;
+    thr_c = t.contrast;
+    if (civ == 0 && lane == 0) {
+      p.stats[view].thr_white = t.white;
+      p.stats[view].thr_contrast = t.contrast;
+      p.stats[view].noise_floor = t.noise_floor;
+      p.stats[view].dynamic_range = t.dynamic_range;
+    }
+  }
+  const int total = civ < p.cpv ? count_chunk<VEC>(p, gc, view, civ, thr_w, thr_c, lane) : 0;
+  if (!(p.mode & M_CODES)) return;  // uniform: no barrier below
+  if (lane == 0) s_sum[wid] = total;
   __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {  // inclusive scan of the chunk sums
-    const long long t = tid >= d ? s_part[tid - d] : 0ll;
-    __syncthreads();
-    s_part[tid] += t;
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) t += s_sum[w];
+    p.block_sums[static_cast<int64_t>(view) * gridDim.x + blockIdx.x] = t;
   }
-  long long run = tid ? s_part[tid - 1] : 0ll;
-  for (int64_t i = lo; i < hi; ++i) {
-    if (p.view_offsets && i % p.tiles_per_view == 0) p.view_offsets[i / p.tiles_per_view] = run;
-    p.tile_offsets[i] = run;
-    run += p.tile_counts[i];
-  }
-  if (tid == 1023 && p.view_offsets) p.view_offsets[p.n_views] = s_part[1023];
 }
 
 // ================================================================= k_cloud ====
-// reconstruct_point_cloud's arithmetic (sl_system.py:584-653) for the pixels
-// k_decode marked: exact f64 in the reference's operation order, stored at
-// tile offset + rank, i.e. in np.where order across tiles and views
-// (sl_system.py:601).
+// reconstruct_point_cloud's arithmetic (sl_system.py:584-653) for the points
+// k_count marked, one chunk per wave:
+//   0. the chunk's offset in the merged cloud: the super-block sums before its
+//      super-block + the chunk counts before it inside it (+ earlier launch
+//      groups);
+//   1. records + colour of the lane's 16 pixels (16-byte loads); the lane's
+//      point count and its exclusive prefix over the wave give every point its
+//      rank in the chunk (ascending pixel order, np.where, sl_system.py:601);
+//   2. each point's (pixel, column code) and BGR go to LDS at its rank -- the
+//      chunk's points, compacted;
+//   3. kPipe x 64 points per pass: lane j takes points j, j+64, ...; all their
+//      operand gathers (ray tables or Nc, plane) are issued before any point
+//      is computed, then the exact f64 arithmetic in the reference's operation
+//      order, then the stores at offset + rank (64 consecutive points per store
+//      instruction).
+constexpr int kPipe = 4;
+
+// One chunk (global index gc, output offset base) of k_cloud, by one wave.
 template <int MODE, int VEC>
-__global__ __launch_bounds__(kThreads, 2) void k_cloud(Params p) {
+__device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane,
+                                            uint32_t* s_ent, uint32_t* s_bgr) {
   const int mode = MODE >= 0 ? MODE : p.mode;
-  const bool vload = VEC > 0;
-
-  __shared__ uint16_t s_code[kWaves][kWavePx];  // record16
-  __shared__ uint32_t s_aux[kWaves][kWavePx];   // B | G << 8 | R << 16
-  __shared__ int s_wsum[kWaves];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
+  const bool vec = VEC > 0;
+  const int view = static_cast<int>(gc / p.cpv);
+  const int civ = static_cast<int>(gc - static_cast<int64_t>(view) * p.cpv);
   const int64_t HW = p.HW;
-  const int view = static_cast<int>(blockIdx.x / p.tiles_per_view);
-  const int64_t lt = blockIdx.x - static_cast<int64_t>(view) * p.tiles_per_view;
-  const long long tile_base = p.tile_offsets[blockIdx.x];  // issued early, used after the scan
+  const int64_t cpx = static_cast<int64_t>(civ) * kChunk;  // chunk's first pixel
+  const int64_t px0 = cpx + lane * kPx;
+  const int n_px = static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx));
+  const int64_t pxl = n_px > 0 ? px0 : 0;
+  __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads come first
 
-  // ============ A) streaming layout: records + colour -> LDS rows ============
+  // ---- 1. records + colour, streaming layout ----
+  uint32_t d[kPx / 2];
   {
-    const int64_t px0 = lt * kTile + static_cast<int64_t>(tid) * kPx;
-    const int n_px = static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx));
-    const int64_t px_ld = n_px > 0 ? px0 : 0;
-    const uint16_t* src = p.codes + view * HW + px_ld;
-    uint32_t d[kPx / 2];
-    if (vload) {
+    const uint16_t* src = p.codes + view * HW + pxl;
+    if (vec) {
       const uint4 a = reinterpret_cast<const uint4*>(src)[0];
       const uint4 b = reinterpret_cast<const uint4*>(src)[1];
       d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
@@ -730,188 +789,202 @@ __global__ __launch_bounds__(kThreads, 2) void k_cloud(Params p) {
         d[i] = lo | (hi << 16);
       }
     }
-    // colour: BGR texture, or the white plane replicated (the colour imread of
-    // a single-channel file 0, sl_system.py:580)
-    uint4 tq[3];
-    if (p.tex != nullptr) {
-      const uint8_t* t = p.tex + view * p.tex_vs + 3 * px_ld;
-      tq[0] = ld16(t, 3 * n_px, vload);
-      tq[1] = ld16(t + 16, 3 * n_px - 16, vload);
-      tq[2] = ld16(t + 32, 3 * n_px - 32, vload);
-    } else {
-      const uint4 wq = ld16(p.stack + view * p.stack_vs + px_ld, n_px, vload);
-      uint32_t t[12];
-#pragma unroll
-      for (int i = 0; i < 12; ++i) t[i] = 0u;
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) {
-        const uint32_t wv = byte_of(wq, k);
-#pragma unroll
-        for (int c = 0; c < 3; ++c) t[(3 * k + c) >> 2] |= wv << (8 * ((3 * k + c) & 3));
-      }
-      tq[0] = make_uint4(t[0], t[1], t[2], t[3]);
-      tq[1] = make_uint4(t[4], t[5], t[6], t[7]);
-      tq[2] = make_uint4(t[8], t[9], t[10], t[11]);
-    }
-    uint16_t* lc = &s_code[wid][lane * kPx];
-    uint32_t* la = &s_aux[wid][lane * kPx];
-    if (n_px < kPx) {  // tail pixels are not points
-#pragma unroll
-      for (int k = 0; k < kPx; ++k)
-        if (k >= n_px) d[k >> 1] &= ~(0xffffu << (16 * (k & 1)));
-    }
-    *reinterpret_cast<uint4*>(lc) = make_uint4(d[0], d[1], d[2], d[3]);
-    *reinterpret_cast<uint4*>(lc + 8) = make_uint4(d[4], d[5], d[6], d[7]);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      uint32_t aw[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = 4 * w + e, b = 3 * k;
-        aw[e] = byte_of(tq[b >> 4], b & 15) | (byte_of(tq[(b + 1) >> 4], (b + 1) & 15) << 8) |
-                (byte_of(tq[(b + 2) >> 4], (b + 2) & 15) << 16);
-      }
-      *reinterpret_cast<uint4*>(la + 4 * w) = make_uint4(aw[0], aw[1], aw[2], aw[3]);
-    }
   }
-  __syncthreads();
-
-  // ============ B) interleaved layout: pixel k*64 + lane of the wave ============
-  // ranks: bit k of `mine` = this lane's pixel is a point; rel[k] = its rank
-  // among the wave's points of steps <= k; bit k of `steps` = step k has one.
-  unsigned mine = 0u, steps = 0u;
-  uint32_t rel[kPx];
-  int total_w = 0;
-#pragma unroll
-  for (int k = 0; k < kPx; ++k) {
-    const bool pt = (s_code[wid][64 * k + lane] >> 15) & 1u;
-    const unsigned long long m = __ballot(pt);
-    rel[k] = static_cast<uint32_t>(total_w) +
-             __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
-                                       __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-    mine |= pt ? (1u << k) : 0u;
-    steps |= m ? (1u << k) : 0u;
-    total_w += __popcll(m);
+  // colour: BGR texture, or the white plane replicated (the colour imread of a
+  // single-channel file 0, sl_system.py:580)
+  uint4 tq[3];
+  const bool has_tex = p.tex != nullptr;
+  if (has_tex) {
+    const uint8_t* t = p.tex + view * p.tex_vs + 3 * pxl;
+    tq[0] = ld16(t, 3 * n_px, vec);
+    tq[1] = ld16(t + 16, 3 * n_px - 16, vec);
+    tq[2] = ld16(t + 32, 3 * n_px - 32, vec);
+  } else {
+    tq[0] = ld16(p.stack + view * p.stack_vs + pxl, n_px, vec);
+    tq[1] = tq[2] = make_uint4(0u, 0u, 0u, 0u);
   }
-  if (lane == 0) s_wsum[wid] = total_w;
-  __syncthreads();
-  long long base = tile_base;
-#pragma unroll
-  for (int w = 0; w < kWaves; ++w) base += (w < wid) ? s_wsum[w] : 0;
+  // the lane's 16 point bits (k_count): bits [16 l, 16 l + 16) of the chunk's mask
+  const uint32_t ptbits =
+      static_cast<uint32_t>(p.ptmask[gc * kPx + (lane >> 2)] >> (16 * (lane & 3))) & 0xffffu;
+  const int n_l = __popc(ptbits);
+  const int incl = wave_incl_scan(n_l, lane);
+  const int total = __shfl(incl, 63, 64);
+  if (lane == 0 && civ == 0) p.view_offsets[view] = base;
+  if (p.dbg & 8) {  // measurement only: stop after the loads and the rank scan
+    if (total == -1) p.bgr[0] = static_cast<uint8_t>(d[0] ^ tq[0].x ^ tq[1].y ^ tq[2].z);
+    return;
+  }
 
-  // r = (x, y, 1) / sqrt((x*x + y*y) + 1) (sl_system.py:614-621), plane of the
-  // clipped code (:624-633), den = (n0 r0 + n1 r1) + n2 r2 (:638),
-  // t = -(n.Oc + d) / den (:639, :643), P = Oc + r t (:648); optional pose.
-  // Groups of four steps are computed branch-free so their chains interleave,
-  // and software-pipelined: the operands of group g+1 are loaded before the
-  // points of group g are stored, because vmcnt counts loads and stores in
-  // one in-order queue -- a load issued after a store makes its wait also
-  // wait for that store.
-  const int64_t wpx = lt * kTile + static_cast<int64_t>(wid) * kWavePx + lane;
-  const int W = p.W;
-  const double* pose = p.poses ? p.poses + 16 * view : nullptr;
-  struct Ops {
-    double r0[4], r1[4], r2[4];  // rays (Nc) or x, y, - (pinhole)
-    double4 pl[4];
-  };
-  int u = static_cast<int>(min<int64_t>(wpx, HW - 1) % W);
-  int v = static_cast<int>(min<int64_t>(wpx, HW - 1) / W);
-  auto fetch = [&](int g, Ops& op) {
+  // ---- 2. compacted entries in LDS ----
+  {
+    int idx = incl - n_l;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int k = g + e;
-      if (mode & M_NC) {
-        const int64_t q = min<int64_t>(wpx + 64 * k, HW - 1);
-        op.r0[e] = p.nc_rays[q];
-        op.r1[e] = p.nc_rays[HW + q];
-        op.r2[e] = p.nc_rays[2 * HW + q];
+    for (int k = 0; k < kPx; ++k) {
+      const uint32_t code = (d[k >> 1] >> (16 * (k & 1))) & 0x7fffu;
+      uint32_t bgr;
+      if (has_tex) {
+        const int b = 3 * k;
+        bgr = byte_of(tq[b >> 4], b & 15) | (byte_of(tq[(b + 1) >> 4], (b + 1) & 15) << 8) |
+              (byte_of(tq[(b + 2) >> 4], (b + 2) & 15) << 16);
       } else {
-        op.r0[e] = p.xn[u];
-        op.r1[e] = p.yn[v];
+        bgr = byte_of(tq[0], k) * 0x010101u;
       }
-      op.pl[e] = p.planes[s_code[wid][64 * k + lane] & 0x7fffu];
-      step64(u, v, W, p.H, vload);
+      if ((ptbits >> k) & 1u) {
+        s_ent[idx] = static_cast<uint32_t>(lane * kPx + k) | (code << 10);
+        s_bgr[idx] = bgr;
+      }
+      idx += (ptbits >> k) & 1u;
     }
-  };
-  Ops cur, nxt;
-  fetch(0, cur);
-#pragma unroll
-  for (int g = 0; g < kPx; g += 4) {
-    if (g + 4 < kPx) fetch(g + 4, nxt);
-    if (((steps >> g) & 0xfu) != 0u && !(p.dbg & 4)) {
-      double X[4], Y[4], Z[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (p.dbg & 16) {  // measurement only: stores without any point math
-          X[e] = cur.r0[e];
-          Y[e] = cur.r1[e];
-          Z[e] = cur.pl[e].w;
-          continue;
-        }
-        if (p.dbg & 32) {  // measurement only: f32 stand-in for the f64 math
-          const float x = static_cast<float>(cur.r0[e]), y = static_cast<float>(cur.r1[e]);
-          const float in = __frsqrt_rn(x * x + y * y + 1.0f);
-          const float4 pf = make_float4(cur.pl[e].x, cur.pl[e].y, cur.pl[e].z, cur.pl[e].w);
-          const float tt = -pf.w / ((pf.x * x + pf.y * y + pf.z) * in);
-          X[e] = x * in * tt;
-          Y[e] = y * in * tt;
-          Z[e] = in * tt;
-          continue;
-        }
-        double r0, r1, r2;
-        if (mode & M_NC) {
-          r0 = cur.r0[e];
-          r1 = cur.r1[e];
-          r2 = cur.r2[e];
-        } else {
-          const double x = cur.r0[e], y = cur.r1[e];
-          const double nrm = sqrt((x * x + y * y) + 1.0);
-          r0 = x / nrm;
-          r1 = y / nrm;
-          r2 = 1.0 / nrm;
-        }
-        const double4 pl = cur.pl[e];
-        const double den = (pl.x * r0 + pl.y * r1) + pl.z * r2;
-        const double num = ((pl.x * p.o0 + pl.y * p.o1) + pl.z * p.o2) + pl.w;
-        const double t = -num / den;
-        X[e] = p.o0 + r0 * t;
-        Y[e] = p.o1 + r1 * t;
-        Z[e] = p.o2 + r2 * t;
-        if (pose) {
-          const double X2 = ((pose[0] * X[e] + pose[1] * Y[e]) + pose[2] * Z[e]) + pose[3];
-          const double Y2 = ((pose[4] * X[e] + pose[5] * Y[e]) + pose[6] * Z[e]) + pose[7];
-          const double Z2 = ((pose[8] * X[e] + pose[9] * Y[e]) + pose[10] * Z[e]) + pose[11];
-          X[e] = X2;
-          Y[e] = Y2;
-          Z[e] = Z2;
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = g + e;
-        if ((mine >> k) & 1u) {
-          const long long o = base + rel[k];
-          if (mode & M_XYZ64) {
-            double* xyz = static_cast<double*>(p.xyz) + 3 * o;
-            xyz[0] = X[e];
-            xyz[1] = Y[e];
-            xyz[2] = Z[e];
-          } else {
-            float* xyz = static_cast<float*>(p.xyz) + 3 * o;
-            xyz[0] = static_cast<float>(X[e]);
-            xyz[1] = static_cast<float>(Y[e]);
-            xyz[2] = static_cast<float>(Z[e]);
-          }
-          const uint32_t aux = s_aux[wid][64 * k + lane];
-          uint8_t* cc = p.bgr + 3 * o;
-          cc[0] = static_cast<uint8_t>(aux);
-          cc[1] = static_cast<uint8_t>(aux >> 8);
-          cc[2] = static_cast<uint8_t>(aux >> 16);
-        }
-      }
-    }
-    cur = nxt;
   }
+  __builtin_amdgcn_wave_barrier();
+  if (p.dbg & 16) return;  // measurement only: stop after the LDS compaction
+
+  // ---- 3. points ----
+  // r = (x, y, 1) / sqrt((x*x + y*y) + 1) (sl_system.py:614-621) or Nc
+  // (:605-606), plane of the clipped code (:624-633), den = (n0 r0 + n1 r1) +
+  // n2 r2 (:638), t = -(n.Oc + d) / den (:639, :643; n.Oc + d per plane,
+  // precomputed in the same order), P = Oc + r t (:648); optional pose.
+  const int W = p.W;
+  const int u_c = static_cast<int>(cpx % W);
+  const int v_c = static_cast<int>(cpx / W);
+  const double* pose = p.poses ? p.poses + 16 * view : nullptr;
+  const bool f64out = (mode & M_XYZ64) != 0;
+  const int dbg = p.dbg;
+  for (int j0 = 0; j0 < total; j0 += 64 * kPipe) {
+    double ra[kPipe], rb[kPipe], rcz[kPipe];  // pinhole: x, y, -; Nc: r0, r1, r2
+    double4 pl[kPipe];
+    uint32_t bgr[kPipe];
+#pragma unroll
+    for (int i = 0; i < kPipe; ++i) {
+      const int j = min(j0 + 64 * i + lane, total - 1);  // past the end: repeat the last point
+      const uint32_t e = s_ent[j];
+      bgr[i] = s_bgr[j];
+      const int local = static_cast<int>(e & 1023u);
+      const int c = static_cast<int>(e >> 10);
+      if (dbg & 4) {
+        ra[i] = 0.25 + local;
+        rb[i] = 0.5;
+        rcz[i] = 1.0;
+        pl[i] = make_double4(0.1, 0.2, 0.9, -500.0 - c);
+        continue;
+      }
+      if (mode & M_NC) {
+        const int64_t q = cpx + local;
+        ra[i] = p.nc_rays[q];
+        rb[i] = p.nc_rays[HW + q];
+        rcz[i] = p.nc_rays[2 * HW + q];
+      } else {
+        int uu = u_c + local, vv = v_c;
+        while (uu >= W) {
+          uu -= W;
+          ++vv;
+        }
+        ra[i] = p.xn[uu];
+        rb[i] = p.yn[vv];
+      }
+      pl[i] = p.planes[c];
+    }
+    double X[kPipe], Y[kPipe], Z[kPipe];
+#pragma unroll
+    for (int i = 0; i < kPipe; ++i) {
+      if (dbg & 1) {
+        X[i] = ra[i];
+        Y[i] = rb[i];
+        Z[i] = pl[i].w;
+        continue;
+      }
+      double r0, r1, r2;
+      if (mode & M_NC) {
+        r0 = ra[i];
+        r1 = rb[i];
+        r2 = rcz[i];
+      } else {
+        const double x = ra[i], y = rb[i];
+        const double nrm = sqrt((x * x + y * y) + 1.0);
+        r0 = x / nrm;
+        r1 = y / nrm;
+        r2 = 1.0 / nrm;
+      }
+      const double den = (pl[i].x * r0 + pl[i].y * r1) + pl[i].z * r2;
+      const double t = -pl[i].w / den;
+      X[i] = p.o0 + r0 * t;
+      Y[i] = p.o1 + r1 * t;
+      Z[i] = p.o2 + r2 * t;
+      if (pose) {
+        const double X2 = ((pose[0] * X[i] + pose[1] * Y[i]) + pose[2] * Z[i]) + pose[3];
+        const double Y2 = ((pose[4] * X[i] + pose[5] * Y[i]) + pose[6] * Z[i]) + pose[7];
+        const double Z2 = ((pose[8] * X[i] + pose[9] * Y[i]) + pose[10] * Z[i]) + pose[11];
+        X[i] = X2;
+        Y[i] = Y2;
+        Z[i] = Z2;
+      }
+    }
+    if (dbg & 2) continue;
+#pragma unroll
+    for (int i = 0; i < kPipe; ++i) {
+      const int j = j0 + 64 * i + lane;
+      if (j < total) {
+        const long long o = base + j;
+        if (f64out) {
+          double* xyz = static_cast<double*>(p.xyz) + 3 * o;
+          xyz[0] = X[i];
+          xyz[1] = Y[i];
+          xyz[2] = Z[i];
+        } else {
+          float* xyz = static_cast<float*>(p.xyz) + 3 * o;
+          xyz[0] = static_cast<float>(X[i]);
+          xyz[1] = static_cast<float>(Y[i]);
+          xyz[2] = static_cast<float>(Z[i]);
+        }
+        uint8_t* cc = p.bgr + 3 * o;
+        cc[0] = static_cast<uint8_t>(bgr[i]);
+        cc[1] = static_cast<uint8_t>(bgr[i] >> 8);
+        cc[2] = static_cast<uint8_t>(bgr[i] >> 16);
+      }
+    }
+  }
+}
+
+
+// k_cloud: one chunk per wave, grid as k_count.  The workgroup's output
+// offset is the sum of k_count's block sums before it (+ the earlier launch
+// groups of the call); each wave adds the counts of the chunks before it in
+// the workgroup.
+constexpr int kPrefixBatch = 4;
+
+template <int MODE, int VEC>
+__global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
+  __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
+  __shared__ uint32_t s_bgr[kWaves][kChunk];  // their B | G << 8 | R << 16
+  __shared__ long long s_wred[kWaves];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int view = blockIdx.y;
+  const int civ = blockIdx.x * kWaves + wid;
+  const int64_t b = static_cast<int64_t>(view) * gridDim.x + blockIdx.x;  // block index in the launch
+  // ---- block offset: all loads of a batch in flight together ----
+  long long acc = 0;
+  for (int64_t t0 = 0; t0 < b; t0 += kPrefixBatch * kThreads) {
+    int v[kPrefixBatch];
+#pragma unroll
+    for (int i = 0; i < kPrefixBatch; ++i) v[i] = p.block_sums[min<int64_t>(t0 + i * kThreads + tid, b - 1)];
+#pragma unroll
+    for (int i = 0; i < kPrefixBatch; ++i) acc += (t0 + i * kThreads + tid < b) ? v[i] : 0;
+  }
+  const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
+  const int before = (lane < wid && civ < p.cpv) ? p.chunk_counts[gc - wid + lane] : 0;  // earlier waves' chunks
+  acc = wave_sum64(acc);
+  if (lane == 0) s_wred[wid] = acc;
+  __syncthreads();
+  long long base = p.base_in ? *p.base_in : 0ll;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) base += s_wred[w];
+  base += wave_sum(before);
+  if (civ >= p.cpv) return;
+  if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1)
+    p.view_offsets[p.n_views] = base + p.chunk_counts[gc];
+  cloud_chunk<MODE, VEC>(p, gc, base, lane, &s_ent[wid][0], &s_bgr[wid][0]);
 }
 
 }  // namespace
@@ -925,27 +998,30 @@ struct sl_ctx {
   bool has_calib = false;
   int H = 0, W = 0, Wp = 0;
   double Oc[3] = {0, 0, 0};
-  double* d_planes = nullptr;
+  double* d_planes = nullptr;  // [Wp] (n0, n1, n2, n.Oc + d)
   double* d_xn = nullptr;
   double* d_yn = nullptr;
   float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H]
   double* d_nc = nullptr;
   // scratch
-  Header* d_hdr = nullptr;
   ViewStats* d_stats = nullptr;
-  int64_t cap_views = 0;
-  unsigned* d_part = nullptr;
-  int64_t cap_part = 0;
-  int* d_tile_counts = nullptr;
-  int64_t cap_tc = 0;
-  long long* d_tile_offsets = nullptr;
-  int64_t cap_to = 0;
-  uint16_t* d_codes = nullptr;  // k_decode -> k_cloud records
+  int64_t cap_stats = 0;
+  unsigned* d_hist[2] = {nullptr, nullptr};  // per-view histograms, parity double-buffered
+  int64_t cap_hist[2] = {0, 0};
+  int64_t hist_dirty[2] = {0, 0};  // leading views of each buffer that may be non-zero
+  int par = 0;                     // buffer the next adaptive launch accumulates into
+  int* d_chunk_counts = nullptr;
+  int64_t cap_cc = 0;
+  int* d_block_sums = nullptr;
+  int64_t cap_bs = 0;
+  uint64_t* d_ptmask = nullptr;
+  int64_t cap_ptmask = 0;
+  uint16_t* d_codes = nullptr;  // k_decode -> k_count / k_cloud records
   int64_t cap_codes = 0;
   int last_views = 0;
   int dbg = 0;
-  // optional per-launch HIP-event timing of k_stats / k_decode / k_cloud
-  std::vector<hipEvent_t> prof_ev;  // kProfEv events per launch slot
+  // optional per-call HIP-event timing of k_decode / k_count / k_cloud
+  std::vector<hipEvent_t> prof_ev;  // kProfEv events per call slot
   int prof_n = 0;
 };
 
@@ -981,30 +1057,41 @@ int grow(sl_ctx* c, T** ptr, int64_t* cap, int64_t need) {
   return SL_OK;
 }
 
-int ensure_scratch(sl_ctx* c, int64_t views, int64_t tiles) {
-  int r = grow(c, &c->d_stats, &c->cap_views, views);
+// scratch for `views` views of `px` pixels each
+int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes) {
+  const int64_t chunks = views * ((px + kChunk - 1) / kChunk);
+  int r = grow(c, &c->d_chunk_counts, &c->cap_cc, chunks);
   if (r) return r;
-  r = grow(c, &c->d_part, &c->cap_part, views * kReps * kSlot);
+  r = grow(c, &c->d_block_sums, &c->cap_bs, views * (((px + kChunk - 1) / kChunk + kWaves - 1) / kWaves));
   if (r) return r;
-  r = grow(c, &c->d_tile_counts, &c->cap_tc, tiles);
+  r = grow(c, &c->d_ptmask, &c->cap_ptmask, chunks * kPx);
   if (r) return r;
-  return grow(c, &c->d_tile_offsets, &c->cap_to, tiles);
+  for (int b = 0; b < 2; ++b) {
+    const int64_t before = c->cap_hist[b];
+    r = grow(c, &c->d_hist[b], &c->cap_hist[b], views * kSlot);
+    if (r) return r;
+    if (c->cap_hist[b] != before) c->hist_dirty[b] = 0;  // fresh (zeroed) allocation
+  }
+  if (codes) return grow(c, &c->d_codes, &c->cap_codes, views * px + 16);
+  return SL_OK;
 }
 
 using KernelFn = void (*)(Params);
-constexpr int kProfEv = 4;  // events per launch: before k_stats, k_decode, k_cloud, after
+constexpr int kProfEv = 4;  // events per call: before k_decode, k_count, k_cloud, after
 
 // k_decode specialisations for the benchmark configurations; everything else
 // (other bit counts, unaligned frames) runs the generic instantiation.
 KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
   if (vec && !(mode & (M_NC | M_FROMMAPS))) {
-    const int mr = M_MAPS | M_ROWS, mrc = M_MAPS | M_ROWS | M_CODES;
+    constexpr int mrch = M_MAPS | M_ROWS | M_CODES | M_HIST, mrh = M_MAPS | M_ROWS | M_HIST,
+                  ch = M_CODES | M_HIST, mrc = M_MAPS | M_ROWS | M_CODES, cc = M_CODES;
+    if (mode == mrch && kc == 11 && kr == 11) return k_decode<11, 11, mrch, 1>;
+    if (mode == mrch && kc == 10 && kr == 0) return k_decode<10, 0, mrch, 1>;
+    if (mode == mrh && kc == 11 && kr == 11) return k_decode<11, 11, mrh, 1>;
+    if (mode == ch && kc == 11) return k_decode<11, 0, ch, 1>;
+    if (mode == ch && kc == 10) return k_decode<10, 0, ch, 1>;
     if (mode == mrc && kc == 11 && kr == 11) return k_decode<11, 11, mrc, 1>;
-    if (mode == mrc && kc == 10 && kr == 10) return k_decode<10, 10, mrc, 1>;
-    if (mode == mrc && kc == 10 && kr == 0) return k_decode<10, 0, mrc, 1>;
-    if (mode == mr && kc == 11 && kr == 11) return k_decode<11, 11, mr, 1>;
-    if (mode == M_CODES && kc == 11) return k_decode<11, 0, M_CODES, 1>;
-    if (mode == M_CODES && kc == 10) return k_decode<10, 0, M_CODES, 1>;
+    if (mode == cc && kc == 11) return k_decode<11, 0, cc, 1>;
   }
   return vec ? k_decode<-1, -1, -1, 1> : k_decode<-1, -1, -1, 0>;
 }
@@ -1016,56 +1103,75 @@ KernelFn pick_cloud(int mode, bool vec) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// Enqueue [k_stats] -> k_decode -> [k_scan -> k_cloud] on stream s.
-// cloud_mode < 0: no cloud.
-int launch(sl_ctx* c, Params& p, bool vec, bool do_stats, int decode_mode, int cloud_mode, hipStream_t s) {
-  const int64_t tiles = static_cast<int64_t>(p.n_views) * p.tiles_per_view;
-  if (tiles >= (1ll << 31)) return fail(c, SL_EINVAL, "too many pixels in one call");
-  int r = ensure_scratch(c, p.n_views, tiles);
+// Enqueue, per launch group of views, k_decode -> k_count [-> k_cloud] on
+// stream s.  decode_mode / count_mode / cloud_mode (< 0: no cloud) are the
+// kernels' mode bits.  Launch groups hold at most kMaxChunks chunks (at least
+// one view); a group's points follow the earlier groups' (base_in).
+int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mode, int cloud_mode,
+           hipStream_t s) {
+  const int64_t cpv = p0.cpv;
+  const int vpg = static_cast<int>(std::max<int64_t>(1, kMaxChunks / cpv));  // views per group
+  const bool adaptive = (decode_mode & M_HIST) != 0;
+  int r = ensure_scratch(c, std::min(vpg, p0.n_views), p0.HW, (decode_mode & M_CODES) != 0);
   if (r) return r;
-  if (decode_mode & M_CODES) {
-    r = grow(c, &c->d_codes, &c->cap_codes, static_cast<int64_t>(p.n_views) * p.HW + 16);
-    if (r) return r;
-  }
-  p.stats = c->d_stats;
-  p.part = c->d_part;
-  p.tile_counts = c->d_tile_counts;
-  p.tile_offsets = c->d_tile_offsets;
-  p.hdr = c->d_hdr;
-  p.codes = c->d_codes;
-  c->last_views = p.n_views;
+  r = grow(c, &c->d_stats, &c->cap_stats, p0.n_views);
+  if (r) return r;
+  c->last_views = p0.n_views;
   hipEvent_t* ev = nullptr;
   if (!c->prof_ev.empty() && kProfEv * (c->prof_n + 1) <= static_cast<int>(c->prof_ev.size()))
     ev = &c->prof_ev[kProfEv * c->prof_n++];
   if (ev) HIP_TRY(c, hipEventRecord(ev[0], s));
-  if (do_stats) {
-    const int bx = static_cast<int>(std::max<int64_t>(
-        1, std::min<int64_t>({static_cast<int64_t>(p.tiles_per_view), int64_t{kStatBlocks},
-                              std::max<int64_t>(1, 2048 / p.n_views)})));
-    int vec_flag = vec ? 1 : 0;
-    void* args[] = {&p, &vec_flag};
-    HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(k_stats), dim3(bx, p.n_views), dim3(kThreads), args,
-                               0, s));
-  }
-  if (ev) HIP_TRY(c, hipEventRecord(ev[1], s));
-  {
-    Params q = p;
-    q.mode = decode_mode;
-    void* args[] = {&q};
-    KernelFn fn = pick_decode(q.kc, (decode_mode & M_ROWS) ? q.kr : 0, decode_mode, vec);
-    HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(static_cast<unsigned>(tiles)),
-                               dim3(kThreads), args, 0, s));
-  }
-  if (ev) HIP_TRY(c, hipEventRecord(ev[2], s));
-  if (cloud_mode >= 0) {
-    void* sargs[] = {&p};
-    HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(k_scan), dim3(1), dim3(1024), sargs, 0, s));
-    Params q = p;
-    q.mode = cloud_mode;
-    void* args[] = {&q};
-    KernelFn fn = pick_cloud(cloud_mode, vec);
-    HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(static_cast<unsigned>(tiles)),
-                               dim3(kThreads), args, 0, s));
+  for (int v0 = 0; v0 < p0.n_views; v0 += vpg) {
+    const int nv = std::min(vpg, p0.n_views - v0);
+    Params p = p0;
+    p.n_views = nv;
+    p.n_chunks = static_cast<int64_t>(nv) * cpv;
+    if (p.stack) p.stack += v0 * p.stack_vs;
+    if (p.tex) p.tex += v0 * p.tex_vs;
+    if (p.in_col) p.in_col += v0 * p.HW;
+    if (p.in_mask) p.in_mask += v0 * p.HW;
+    if (p.col_out) p.col_out += v0 * p.HW;
+    if (p.row_out) p.row_out += v0 * p.HW;
+    if (p.mask_out) p.mask_out += v0 * p.HW;
+    if (p.poses) p.poses += 16 * v0;
+    if (p.view_offsets) p.view_offsets += v0;
+    p.base_in = (v0 > 0 && p.view_offsets) ? p.view_offsets : nullptr;
+    p.stats = c->d_stats + v0;
+    p.codes = c->d_codes;
+    p.ptmask = c->d_ptmask;
+    p.chunk_counts = c->d_chunk_counts;
+    p.block_sums = c->d_block_sums;
+    if (adaptive) {
+      const int a = c->par, b = 1 - c->par;
+      if (c->hist_dirty[a] > 0)
+        HIP_TRY(c, hipMemsetAsync(c->d_hist[a], 0, sizeof(unsigned) * kSlot * c->hist_dirty[a], s));
+      p.hist = c->d_hist[a];
+      p.hist_zero = c->d_hist[b];
+      c->hist_dirty[a] = nv;
+      if (c->hist_dirty[b] <= nv) c->hist_dirty[b] = 0;
+      c->par = b;
+    }
+    const dim3 grid(static_cast<unsigned>((cpv + kWaves - 1) / kWaves), static_cast<unsigned>(nv));
+    {
+      p.mode = decode_mode;
+      void* args[] = {&p};
+      KernelFn fn = pick_decode(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode, vec);
+      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(kThreads), args, 0, s));
+    }
+    if (ev && v0 == 0) HIP_TRY(c, hipEventRecord(ev[1], s));
+    {
+      p.mode = count_mode;
+      void* args[] = {&p};
+      const void* fn = vec ? reinterpret_cast<const void*>(k_count<1>) : reinterpret_cast<const void*>(k_count<0>);
+      HIP_TRY(c, hipLaunchKernel(fn, grid, dim3(kThreads), args, 0, s));
+    }
+    if (ev && v0 == 0) HIP_TRY(c, hipEventRecord(ev[2], s));
+    if (cloud_mode >= 0) {
+      p.mode = cloud_mode;
+      void* args[] = {&p};
+      KernelFn fn = pick_cloud(cloud_mode, vec);
+      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(kThreads), args, 0, s));
+    }
   }
   if (ev) HIP_TRY(c, hipEventRecord(ev[3], s));
   return SL_OK;
@@ -1082,11 +1188,8 @@ int sl_ctx_create(int device, sl_ctx** out) {
   *out = nullptr;
   sl_ctx* c = new sl_ctx();
   c->device = device;
-  if (const char* d = getenv("SLGPU_DEBUG")) c->dbg = atoi(d);
-  hipError_t e = hipSetDevice(device);
-  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&c->d_hdr), sizeof(Header));
-  if (e == hipSuccess) e = hipMemset(c->d_hdr, 0, sizeof(Header));
-  if (e != hipSuccess) {
+  if (const char* d = getenv("SLGPU_DEBUG")) c->dbg = atoi(d);  // measurement-only ablations
+  if (hipSetDevice(device) != hipSuccess) {
     delete c;
     return SL_EHIP;
   }
@@ -1099,10 +1202,10 @@ void sl_ctx_destroy(sl_ctx* c) {
   (void)hipSetDevice(c->device);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (void* ptr : {static_cast<void*>(c->d_planes), static_cast<void*>(c->d_xn), static_cast<void*>(c->d_yn),
-                    static_cast<void*>(c->d_nc), static_cast<void*>(c->d_hdr), static_cast<void*>(c->d_stats),
-                    static_cast<void*>(c->d_f32), static_cast<void*>(c->d_codes),
-                    static_cast<void*>(c->d_part),
-                    static_cast<void*>(c->d_tile_counts), static_cast<void*>(c->d_tile_offsets)})
+                    static_cast<void*>(c->d_nc), static_cast<void*>(c->d_stats), static_cast<void*>(c->d_f32),
+                    static_cast<void*>(c->d_codes), static_cast<void*>(c->d_hist[0]),
+                    static_cast<void*>(c->d_hist[1]), static_cast<void*>(c->d_ptmask),
+                    static_cast<void*>(c->d_block_sums), static_cast<void*>(c->d_chunk_counts)})
     if (ptr) (void)hipFree(ptr);
   delete c;
 }
@@ -1112,7 +1215,10 @@ const char* sl_ctx_last_error(const sl_ctx* c) { return c ? c->err.c_str() : "nu
 int sl_ctx_reserve(sl_ctx* c, int64_t max_views, int64_t max_px) {
   if (!c || max_views < 1 || max_px < 1) return fail(c, SL_EINVAL, "sl_ctx_reserve: bad sizes");
   HIP_TRY(c, hipSetDevice(c->device));
-  return ensure_scratch(c, max_views, max_views * ((max_px + kTile - 1) / kTile));
+  const int64_t vpg = std::max<int64_t>(1, kMaxChunks / ((max_px + kChunk - 1) / kChunk));
+  int r = ensure_scratch(c, std::min(vpg, max_views), max_px, true);
+  if (r) return r;
+  return grow(c, &c->d_stats, &c->cap_stats, max_views);
 }
 
 int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, const double* planes,
@@ -1120,7 +1226,7 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
   if (!c) return SL_EINVAL;
   if (H < 1 || W < 1 || Wp < 1 || !K || !Oc || !planes)
     return fail(c, SL_EINVAL, "sl_set_calib: bad arguments");
-  if (Wp > 32768) return fail(c, SL_EINVAL, "sl_set_calib: at most 32768 projector columns");
+  if (Wp > kMaxWp) return fail(c, SL_EINVAL, "sl_set_calib: at most 32768 projector columns");
   HIP_TRY(c, hipSetDevice(c->device));
   const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
   // (x_v - cx) / fx and (y_v - cy) / fy with integer pixel coordinates
@@ -1139,13 +1245,24 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
         if (memcmp(&r[k], &Nc[k * HW + q], sizeof(double)) != 0) use_nc = true;
     }
   }
+  // per plane: (n0, n1, n2, n.Oc + d) -- numer of sl_system.py:639, in its
+  // operation order ((n0 o0 + n1 o1) + n2 o2) + d
+  std::vector<double> pl(4 * static_cast<size_t>(Wp));
+  for (int i = 0; i < Wp; ++i) {
+    const double* s = planes + 4 * static_cast<size_t>(i);
+    pl[4 * i] = s[0];
+    pl[4 * i + 1] = s[1];
+    pl[4 * i + 2] = s[2];
+    pl[4 * i + 3] = ((s[0] * Oc[0] + s[1] * Oc[1]) + s[2] * Oc[2]) + s[3];
+  }
   for (double* ptr : {c->d_planes, c->d_xn, c->d_yn, c->d_nc})
     if (ptr) HIP_TRY(c, hipFree(ptr));
   if (c->d_f32) HIP_TRY(c, hipFree(c->d_f32));
   c->d_planes = c->d_xn = c->d_yn = c->d_nc = nullptr;
   c->d_f32 = nullptr;
+  c->has_calib = false;
   HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_planes), sizeof(double) * 4 * Wp));
-  HIP_TRY(c, hipMemcpy(c->d_planes, planes, sizeof(double) * 4 * Wp, hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->d_planes, pl.data(), sizeof(double) * 4 * Wp, hipMemcpyHostToDevice));
   HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_xn), sizeof(double) * W));
   HIP_TRY(c, hipMemcpy(c->d_xn, xn.data(), sizeof(double) * W, hipMemcpyHostToDevice));
   HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_yn), sizeof(double) * H));
@@ -1192,7 +1309,8 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.H = H;
   p.W = W;
   p.n_views = n_views;
-  p.tiles_per_view = static_cast<int>((p.HW + kTile - 1) / kTile);
+  p.cpv = static_cast<int>((p.HW + kChunk - 1) / kChunk);
+  p.n_chunks = static_cast<int64_t>(n_views) * p.cpv;
   p.Wp = c->Wp;
   p.planes = reinterpret_cast<const double4*>(c->d_planes);
   p.xn = c->d_xn;
@@ -1248,7 +1366,6 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   p.nr = nr;
   p.kc = std::min(nc, pairs);
   p.kr = pairs - p.kc;
-  p.mask_mode = mask_mode;
   p.poses = poses;
   p.col_out = col_out;
   p.row_out = row_out;
@@ -1257,13 +1374,15 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   p.bgr = bgr;
   p.view_offsets = view_offsets;
   const int nc_bit = (xyz && c->d_nc) ? M_NC : 0;
-  const int decode_mode = (maps ? (M_MAPS | M_ROWS) : 0) | (xyz ? M_CODES : 0) | nc_bit;
+  const int hist_bit = mask_mode == SL_MASK_ADAPTIVE ? M_HIST : 0;
+  const int decode_mode = (maps ? (M_MAPS | M_ROWS) : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit;
+  const int count_mode = (maps ? M_MAPS : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit;
   const int cloud_mode = xyz ? ((xyz_dtype == SL_XYZ_F64 ? M_XYZ64 : 0) | nc_bit) : -1;
   const bool vec = (W % 16 == 0) && W >= 64 && aligned16(stack) && (stack_vs % 16 == 0) &&
                    (!tex || (aligned16(tex) && tex_vs % 16 == 0)) &&
                    (!maps || (aligned16(col_out) && aligned16(row_out) && aligned16(mask_out)));
   HIP_TRY(c, hipSetDevice(c->device));
-  return launch(c, p, vec, mask_mode == SL_MASK_ADAPTIVE, decode_mode, cloud_mode, static_cast<hipStream_t>(stream));
+  return launch(c, p, vec, decode_mode, count_mode, cloud_mode, static_cast<hipStream_t>(stream));
 }
 
 int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, const uint8_t* tex,
@@ -1281,39 +1400,34 @@ int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, 
   p.in_mask = mask;
   p.tex = tex;
   p.tex_vs = 3 * HW;
-  p.mask_mode = SL_MASK_FIXED;  // unused on this path
   p.poses = poses;
   p.xyz = xyz;
   p.bgr = bgr;
   p.view_offsets = view_offsets;
   const int nc_bit = c->d_nc ? M_NC : 0;
   const int decode_mode = M_FROMMAPS | M_CODES | nc_bit;
+  const int count_mode = M_FROMMAPS | M_CODES | nc_bit;
   const int cloud_mode = (xyz_dtype == SL_XYZ_F64 ? M_XYZ64 : 0) | nc_bit;
   const bool vec = (W % 16 == 0) && W >= 64 && aligned16(col_map) && aligned16(mask) && aligned16(tex);
   HIP_TRY(c, hipSetDevice(c->device));
-  return launch(c, p, vec, false, decode_mode, cloud_mode, static_cast<hipStream_t>(stream));
+  return launch(c, p, vec, decode_mode, count_mode, cloud_mode, static_cast<hipStream_t>(stream));
 }
 
 int sl_sync(sl_ctx* c, void* stream) {
   if (!c) return SL_EINVAL;
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(static_cast<hipStream_t>(stream)));
-  Header h;
-  HIP_TRY(c, hipMemcpy(&h, c->d_hdr, sizeof(Header), hipMemcpyDeviceToHost));
-  if (h.error) {
-    HIP_TRY(c, hipMemset(&c->d_hdr->error, 0, sizeof(unsigned)));
-    return fail(c, SL_ETIMEOUT, "device-side look-back wait expired");
-  }
+  HIP_TRY(c, hipGetLastError());
   return SL_OK;
 }
 
-int sl_profile_enable(sl_ctx* c, int max_launches) {
-  if (!c || max_launches < 0) return SL_EINVAL;
+int sl_profile_enable(sl_ctx* c, int max_calls) {
+  if (!c || max_calls < 0) return SL_EINVAL;
   HIP_TRY(c, hipSetDevice(c->device));
   for (hipEvent_t e : c->prof_ev) HIP_TRY(c, hipEventDestroy(e));
   c->prof_ev.clear();
   c->prof_n = 0;
-  for (int i = 0; i < kProfEv * max_launches; ++i) {
+  for (int i = 0; i < kProfEv * max_calls; ++i) {
     hipEvent_t e;
     HIP_TRY(c, hipEventCreate(&e));
     c->prof_ev.push_back(e);
@@ -1321,7 +1435,7 @@ int sl_profile_enable(sl_ctx* c, int max_launches) {
   return SL_OK;
 }
 
-int sl_profile_read(sl_ctx* c, double* stats_ms, double* decode_ms, double* cloud_ms, int* launches) {
+int sl_profile_read(sl_ctx* c, double* decode_ms, double* count_ms, double* cloud_ms, int* calls) {
   if (!c) return SL_EINVAL;
   HIP_TRY(c, hipSetDevice(c->device));
   double t[3] = {0.0, 0.0, 0.0};
@@ -1334,10 +1448,10 @@ int sl_profile_read(sl_ctx* c, double* stats_ms, double* decode_ms, double* clou
       t[k] += ms;
     }
   }
-  if (stats_ms) *stats_ms = t[0];
-  if (decode_ms) *decode_ms = t[1];
+  if (decode_ms) *decode_ms = t[0];
+  if (count_ms) *count_ms = t[1];
   if (cloud_ms) *cloud_ms = t[2];
-  if (launches) *launches = c->prof_n;
+  if (calls) *calls = c->prof_n;
   c->prof_n = 0;
   return SL_OK;
 }
