@@ -55,6 +55,46 @@ constexpr int kChunk = 64 * kPx;        // pixels per wave (one chunk)
 #define SLGPU_RING 48
 #endif
 constexpr int kRing = SLGPU_RING;       // stack planes in flight per lane
+#ifndef SLGPU_LOAD_AUX
+#define SLGPU_LOAD_AUX 2
+#endif
+constexpr int kLoadAux = SLGPU_LOAD_AUX;  // cache policy of the stack loads (2 = nt)
+#ifndef SLGPU_NT_MAPS
+#define SLGPU_NT_MAPS 0
+#endif
+constexpr bool kNtMaps = SLGPU_NT_MAPS != 0;  // non-temporal col/row map stores
+
+#ifndef SLGPU_NT_SIDE
+#define SLGPU_NT_SIDE 0
+#endif
+constexpr bool kNtSide = SLGPU_NT_SIDE != 0;  // nt loads of records / texture / white-black in k_count, k_cloud
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ld_side16(const void* p) {
+  if (kNtSide) {
+    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return *reinterpret_cast<const uint4*>(p);
+}
+__device__ __forceinline__ uint2 ld_side8(const void* p) {
+  if (kNtSide) {
+    const v2u v = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+    return make_uint2(v.x, v.y);
+  }
+  return *reinterpret_cast<const uint2*>(p);
+}
+__device__ __forceinline__ uint32_t ld_side4(const void* p) {
+  if (kNtSide) return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
+  return *reinterpret_cast<const uint32_t*>(p);
+}
+typedef int v4i __attribute__((ext_vector_type(4)));
+// 16-byte store of 4 map words at p (16-byte aligned)
+__device__ __forceinline__ void st_map(int32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const v4i v = {static_cast<int>(a), static_cast<int>(b), static_cast<int>(c), static_cast<int>(d)};
+  if (kNtMaps) __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(p));
+  else *reinterpret_cast<v4i*>(p) = v;
+}
 
 // mode bits
 constexpr int M_MAPS = 1;      // k_decode: col/row maps; k_count: mask map
@@ -365,7 +405,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(Params p) {
     const int voff = static_cast<int>(pxl);
     auto ldp = [&](int plane) -> uint4 {
       if (vec) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, plane * static_cast<int>(HW), 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, plane * static_cast<int>(HW), kLoadAux);
         return make_uint4(v[0], v[1], v[2], v[3]);
       }
       return ld16(vbase + pxl + static_cast<int64_t>(plane) * HW, n_px, false);
@@ -458,12 +498,10 @@ __global__ __launch_bounds__(kThreads) void k_decode(Params p) {
     if (mode & M_MAPS) {
       if (vec) {
         if (n_px == kPx) {
-          int4* co = reinterpret_cast<int4*>(p.col_out + o);
-          int4* ro = reinterpret_cast<int4*>(p.row_out + o);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            co[i] = make_int4(col[4 * i], col[4 * i + 1], col[4 * i + 2], col[4 * i + 3]);
-            ro[i] = make_int4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
+            st_map(p.col_out + o + 4 * i, col[4 * i], col[4 * i + 1], col[4 * i + 2], col[4 * i + 3]);
+            st_map(p.row_out + o + 4 * i, row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
           }
         }
       } else {
@@ -563,8 +601,8 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
       wv[s] = bv[s] = 0u;
     } else if (vec) {
       const uint8_t* sp = p.stack + view * p.stack_vs + px;
-      wv[s] = *reinterpret_cast<const uint32_t*>(sp);
-      bv[s] = *reinterpret_cast<const uint32_t*>(sp + HW);
+      wv[s] = ld_side4(sp);
+      bv[s] = ld_side4(sp + HW);
     } else {
       const uint8_t* sp = p.stack + view * p.stack_vs;
       uint32_t a = 0u, b = 0u;
@@ -579,7 +617,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
     }
     if (codes) {
       if (vec) {
-        const uint2 r = *reinterpret_cast<const uint2*>(p.codes + view * HW + px);
+        const uint2 r = ld_side8(p.codes + view * HW + px);
         rc[s][0] = r.x;
         rc[s][1] = r.y;
       } else {
@@ -755,7 +793,10 @@ __global__ __launch_bounds__(kThreads) void k_count(Params p) {
 //      is computed, then the exact f64 arithmetic in the reference's operation
 //      order, then the stores at offset + rank (64 consecutive points per store
 //      instruction).
-constexpr int kPipe = 4;
+#ifndef SLGPU_PIPE
+#define SLGPU_PIPE 4
+#endif
+constexpr int kPipe = SLGPU_PIPE;  // points per lane per pass in k_cloud
 
 // One chunk (global index gc, output offset base) of k_cloud, by one wave.
 template <int MODE, int VEC>
@@ -777,8 +818,8 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   {
     const uint16_t* src = p.codes + view * HW + pxl;
     if (vec) {
-      const uint4 a = reinterpret_cast<const uint4*>(src)[0];
-      const uint4 b = reinterpret_cast<const uint4*>(src)[1];
+      const uint4 a = ld_side16(src);
+      const uint4 b = ld_side16(src + 8);
       d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
       d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
     } else {
@@ -796,9 +837,15 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   const bool has_tex = p.tex != nullptr;
   if (has_tex) {
     const uint8_t* t = p.tex + view * p.tex_vs + 3 * pxl;
-    tq[0] = ld16(t, 3 * n_px, vec);
-    tq[1] = ld16(t + 16, 3 * n_px - 16, vec);
-    tq[2] = ld16(t + 32, 3 * n_px - 32, vec);
+    if (vec) {
+      tq[0] = ld_side16(t);
+      tq[1] = ld_side16(t + 16);
+      tq[2] = ld_side16(t + 32);
+    } else {
+      tq[0] = ld16(t, 3 * n_px, false);
+      tq[1] = ld16(t + 16, 3 * n_px - 16, false);
+      tq[2] = ld16(t + 32, 3 * n_px - 32, false);
+    }
   } else {
     tq[0] = ld16(p.stack + view * p.stack_vs + pxl, n_px, vec);
     tq[1] = tq[2] = make_uint4(0u, 0u, 0u, 0u);
