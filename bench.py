@@ -222,7 +222,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_decode", "kernel_avg_ms": dec_avg_ms,
                          "algorithmic_bytes_per_launch": ab,
-                         "bytes_note": "stack planes read + col/row/mask maps written, per launch"},
+                         "bytes_note": "stack planes read + col/row int32 maps written, per launch (records are overhead)"},
             "path": {"algorithmic_bytes_per_step": path_b,
                      "GBps": path_b / (el / a.steps) / 1e9,
                      "kernel_avg_ms": {"k_decode": dec_avg_ms, "k_count": count_ms / max(nl, 1),

@@ -40,7 +40,7 @@ extern "C" {
                              sl_system.py:553-554                                      */
 #define SL_EHIP (-3)      /* HIP runtime failure -> RuntimeError                        */
 #define SL_ENOCALIB (-4)  /* sl_set_calib not called / shape mismatch -> ValueError       */
-#define SL_ETIMEOUT (-5)  /* a device-side bounded wait expired -> RuntimeError         */
+#define SL_ETIMEOUT (-5)  /* reserved (no device-side waits in this version)             */
 #define SL_ECAPACITY (-6) /* output capacity smaller than the pixel count -> ValueError   */
 
 /* mask_mode */
@@ -122,8 +122,8 @@ int sl_triangulate_maps(sl_ctx* ctx, const int32_t* col_map, const uint8_t* mask
                         const double* poses, void* xyz_out, int xyz_dtype, uint8_t* bgr_out,
                         int64_t out_capacity, int64_t* view_offsets, void* stream);
 
-/* Synchronise `stream` and report device-side failures (SL_ETIMEOUT) of the
- * work enqueued so far on this context.  Blocking. */
+/* Synchronise `stream` and report any HIP failure of the work enqueued so far
+ * on this context.  Blocking. */
 int sl_sync(sl_ctx* ctx, void* stream);
 
 /* Adaptive-mask diagnostics of the last sl_decode_triangulate (blocking):
@@ -133,15 +133,15 @@ int sl_sync(sl_ctx* ctx, void* stream);
 int sl_last_thresholds(sl_ctx* ctx, int view, float* noise_floor, float* dynamic_range,
                        int* thr_white, int* thr_contrast);
 
-/* Timing: with max_launches > 0, each later call (up to that many) records HIP
- * events on its stream around its kernels k_stats, k_decode and k_cloud.
- * 0 disables. */
-int sl_profile_enable(sl_ctx* ctx, int max_launches);
+/* Timing: with max_calls > 0, each later call (up to that many) records HIP
+ * events on its stream before k_decode, k_count, k_cloud and after the call.
+ * 0 disables.  Events between kernels add launch gaps: keep them out of
+ * throughput measurements. */
+int sl_profile_enable(sl_ctx* ctx, int max_calls);
 
-/* Blocking: summed event time (ms) of k_stats, k_decode and k_cloud over the
+/* Blocking: summed event time (ms) of k_decode, k_count and k_cloud over the
  * recorded calls since the last read, and their count; restarts recording. */
-int sl_profile_read(sl_ctx* ctx, double* stats_ms, double* decode_ms, double* cloud_ms,
-                    int* launches);
+int sl_profile_read(sl_ctx* ctx, double* decode_ms, double* count_ms, double* cloud_ms, int* calls);
 
 #ifdef __cplusplus
 }
