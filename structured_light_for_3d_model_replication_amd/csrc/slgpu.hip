@@ -580,8 +580,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(Params p) {
 // and plane gathers of nearby columns.  Every load is issued before any is
 // used (clamped, unconditional addresses).
 template <int VEC>
-__device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view, int civ, int thr_w, int thr_c,
-                                           int lane) {
+__device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view, int civ, int lane) {
   const int mode = p.mode;
   const bool vec = VEC > 0;
   const int64_t HW = p.HW;
@@ -638,6 +637,20 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
     }
   }
 
+  // ---- thresholds (while the loads above are in flight) ----
+  int thr_w = 40, thr_c = 10;  // fixed: multi_point_cloud_process.py:36-38
+  if ((mode & M_HIST) && !(p.dbg & 32)) {
+    const Thresholds t = thresholds_from_hist(p.hist + view * kSlot, HW, lane);
+    thr_w = t.white;
+    thr_c = t.contrast;
+    if (civ == 0 && lane == 0) {
+      p.stats[view].thr_white = t.white;
+      p.stats[view].thr_contrast = t.contrast;
+      p.stats[view].noise_floor = t.noise_floor;
+      p.stats[view].dynamic_range = t.dynamic_range;
+    }
+  }
+
   // ---- mask ----
   uint32_t ok[4];  // bit e: pixel 256 s + 4 lane + e is valid
 #pragma unroll
@@ -672,11 +685,22 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
   float4 pf[4][4];
   float xs[4][4], ys[4];
   int us[4], vs[4];
+  const int u_c = static_cast<int>(cpx % W), v_c = static_cast<int>(cpx / W);  // chunk origin
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int64_t px = min<int64_t>(cpx + 256 * s + 4 * lane, px_hi);
-    us[s] = static_cast<int>(px % W);
-    vs[s] = static_cast<int>(px / W);
+    // pixel (u, v) of cpx + 256 s + 4 lane, 32-bit stepping from the origin;
+    // tail pixels past the frame are clamped to its last 4 (vec) / 1 pixel
+    int u = u_c + 256 * s + 4 * lane, v = v_c;
+    while (u >= W) {
+      u -= W;
+      ++v;
+    }
+    if (v >= p.H) {
+      v = p.H - 1;
+      u = vec ? W - 4 : W - 1;
+    }
+    us[s] = u;
+    vs[s] = v;
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       pf[s][e] = (p.dbg & 128) ? make_float4(0.5f, 0.1f, 0.8f, 0.f)
@@ -701,9 +725,30 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
     uint32_t nib = 0u;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      if (((ok[s] >> e) & 1u) && (p.dbg & 64)) {
+      if (!((ok[s] >> e) & 1u)) continue;
+      if (p.dbg & 64) {
         nib |= 1u << e;
-      } else if ((ok[s] >> e) & 1u) {
+        continue;
+      }
+      if (!nc) {
+        // Cheap sufficient test: with L = |x| + |y| + 1 >= |(x, y, 1)| and
+        // a = |n.(x, y, 1)| in f32 (error < sum|n_i| L 2^-20, inputs' f32
+        // rounding included), a > L (1.001e-6 + sum|n_i| 2^-20) implies
+        // |n.r| > 1.001e-6 for the exact ray, clear of the reference's f64
+        // rounding.  Pixels that fail take the bounded test below.
+        const float4 f = pf[s][e];
+        const float x = xs[s][e], y = vec ? ys[s] : 0.0f;
+        if (vec) {
+          const float a = fabsf(f.x * x + f.y * y + f.z);
+          const float L = fabsf(x) + fabsf(y) + 1.0f;
+          const float nsum = fabsf(f.x) + fabsf(f.y) + fabsf(f.z);
+          if (a > L * (1.001e-6f + nsum * 9.5367431640625e-07f)) {
+            nib |= 1u << e;
+            continue;
+          }
+        }
+      }
+      {
         const int c = static_cast<int>((rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu);
         int u = us[s] + e, v = vs[s];
         if (!vec && u >= W) {
@@ -745,27 +790,18 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
 
 // k_count: one chunk per wave, grid (chunk groups of 4, views); the
 // workgroup's point total goes to block_sums for k_cloud's offsets.
+#ifndef SLGPU_COUNT_WAVES
+#define SLGPU_COUNT_WAVES 1
+#endif
 template <int VEC>
-__global__ __launch_bounds__(kThreads) void k_count(Params p) {
+__global__ __launch_bounds__(kThreads, SLGPU_COUNT_WAVES) void k_count(Params p) {
   __shared__ int s_sum[kWaves];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int view = blockIdx.y;
   const int civ = blockIdx.x * kWaves + wid;
   const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
-  int thr_w = 40, thr_c = 10;  // fixed: multi_point_cloud_process.py:36-38
-  if ((p.mode & M_HIST) && !(p.dbg & 32)) {
-    const Thresholds t = thresholds_from_hist(p.hist + view * kSlot, p.HW, lane);
-    thr_w = t.white;
-    thr_c = t.contrast;
-    if (civ == 0 && lane == 0) {
-      p.stats[view].thr_white = t.white;
-      p.stats[view].thr_contrast = t.contrast;
-      p.stats[view].noise_floor = t.noise_floor;
-      p.stats[view].dynamic_range = t.dynamic_range;
-    }
-  }
-  const int total = civ < p.cpv ? count_chunk<VEC>(p, gc, view, civ, thr_w, thr_c, lane) : 0;
+  const int total = civ < p.cpv ? count_chunk<VEC>(p, gc, view, civ, lane) : 0;
   if (!(p.mode & M_CODES)) return;  // uniform: no barrier below
   if (lane == 0) s_sum[wid] = total;
   __syncthreads();
@@ -797,11 +833,15 @@ __global__ __launch_bounds__(kThreads) void k_count(Params p) {
 #define SLGPU_PIPE 4
 #endif
 constexpr int kPipe = SLGPU_PIPE;  // points per lane per pass in k_cloud
+#ifndef SLGPU_STAGE_OUT
+#define SLGPU_STAGE_OUT 0
+#endif
+constexpr bool kStageOut = SLGPU_STAGE_OUT != 0;  // f32 points leave through an LDS stage
 
 // One chunk (global index gc, output offset base) of k_cloud, by one wave.
 template <int MODE, int VEC>
 __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane,
-                                            uint32_t* s_ent, uint32_t* s_bgr) {
+                                            uint32_t* s_ent, uint32_t* s_bgr, float* s_sxyz, uint8_t* s_scol) {
   const int mode = MODE >= 0 ? MODE : p.mode;
   const bool vec = VEC > 0;
   const int view = static_cast<int>(gc / p.cpv);
@@ -967,6 +1007,35 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
       }
     }
     if (dbg & 2) continue;
+    if (kStageOut && !f64out) {
+      // 64 points at a time through an LDS stage: their 192 xyz words and 192
+      // colour bytes leave as lane-consecutive dword / byte stores
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
+        const int j = j0 + 64 * i + lane;
+        const int n = min(64, total - (j0 + 64 * i));
+        if (n <= 0) break;
+        s_sxyz[3 * lane] = static_cast<float>(X[i]);
+        s_sxyz[3 * lane + 1] = static_cast<float>(Y[i]);
+        s_sxyz[3 * lane + 2] = static_cast<float>(Z[i]);
+        s_scol[3 * lane] = static_cast<uint8_t>(bgr[i]);
+        s_scol[3 * lane + 1] = static_cast<uint8_t>(bgr[i] >> 8);
+        s_scol[3 * lane + 2] = static_cast<uint8_t>(bgr[i] >> 16);
+        __builtin_amdgcn_wave_barrier();
+        const long long o = base + (j - lane);
+        float* xyz = static_cast<float*>(p.xyz) + 3 * o;
+        uint8_t* cc = p.bgr + 3 * o;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          if (64 * k + lane < 3 * n) {
+            xyz[64 * k + lane] = s_sxyz[64 * k + lane];
+            cc[64 * k + lane] = s_scol[64 * k + lane];
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < kPipe; ++i) {
       const int j = j0 + 64 * i + lane;
@@ -992,7 +1061,6 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   }
 }
 
-
 // k_cloud: one chunk per wave, grid as k_count.  The workgroup's output
 // offset is the sum of k_count's block sums before it (+ the earlier launch
 // groups of the call); each wave adds the counts of the chunks before it in
@@ -1003,6 +1071,8 @@ template <int MODE, int VEC>
 __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
   __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
   __shared__ uint32_t s_bgr[kWaves][kChunk];  // their B | G << 8 | R << 16
+  __shared__ float s_sxyz[kWaves][192];       // output stage: 64 points' xyz
+  __shared__ uint8_t s_scol[kWaves][192];     // and their colour bytes
   __shared__ long long s_wred[kWaves];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1031,7 +1101,7 @@ __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
   if (civ >= p.cpv) return;
   if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1)
     p.view_offsets[p.n_views] = base + p.chunk_counts[gc];
-  cloud_chunk<MODE, VEC>(p, gc, base, lane, &s_ent[wid][0], &s_bgr[wid][0]);
+  cloud_chunk<MODE, VEC>(p, gc, base, lane, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0]);
 }
 
 }  // namespace
