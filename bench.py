@@ -35,11 +35,14 @@ from structured_light_for_3d_model_replication_amd import core, parallel, synth 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 CONFIGS = {
-    # name: (H, W, Wp, Hp, rows, views per GPU per step)
-    "c1": (720, 1280, 1024, 768, False, 1),
-    "c2": (2160, 3840, 1920, 1080, True, 1),
-    "c3": (1080, 1920, 1920, 1080, True, 36),
-    "c4": (3000, 4000, 1920, 1080, True, 4),
+    # BASELINE.json configs.  views = views per GPU per step (weak scaling);
+    # maps: also write the col/row/mask maps (what gray_decode returns); pose:
+    # turntable pose epilogue (config 5's merge into one frame).
+    "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0),
+    "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0),
+    "c3": dict(H=1080, W=1920, Wp=1920, Hp=1080, rows=True, views=36, maps=False, pose=False, deg=10.0),
+    "c4": dict(H=3000, W=4000, Wp=1920, Hp=1080, rows=True, views=4, maps=False, pose=False, deg=1.0),
+    "c5": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=4, maps=False, pose=True, deg=1.0),
 }
 
 
@@ -58,21 +61,21 @@ def parse():
     return ap.parse_args()
 
 
-def path_bytes(H, W, n_planes, n_points, maps=True):
-    """SURVEY.md §8(d), whole path: H*W*(2+2(nc+nr)) stack + 3*H*W texture
-    + 15*N_out, + 8*H*W col/row int32 + H*W mask bytes when maps are written."""
+def path_bytes(H, W, read_planes, n_points, maps):
+    """SURVEY.md §8(d), whole path per view: the stack planes the path reads
+    (2 + 2(nc+nr) with maps; 2 + 2 nc for the cloud alone -- row planes are
+    never read, sl_system.py:584-653 uses only col_map) + 3 B/px texture +
+    15 B/point (f32 xyz + BGR) + 9 B/px col/row/mask maps when written."""
     px = H * W
-    b = n_planes * px + 3 * px + 15 * n_points
-    if maps:
-        b += 9 * px
-    return b
+    return read_planes * px + 3 * px + 15 * n_points + (9 * px if maps else 0)
 
 
-def decode_bytes(H, W, n_planes, maps=True):
-    """Algorithmic bytes of one k_decode launch: the stack it streams + the
-    col/row int32 maps it writes (its 2-byte per-pixel records for k_count /
-    k_cloud are overhead, not counted; the mask map is written by k_count)."""
-    return H * W * (n_planes + (8 if maps else 0))
+def decode_bytes(H, W, read_planes, maps):
+    """Algorithmic bytes of one k_decode pass over a view: the stack planes it
+    streams + the col/row int32 maps it writes (its 2-byte per-pixel records
+    for k_count / k_cloud are overhead, not counted; the mask map is written by
+    k_count)."""
+    return H * W * (read_planes + (8 if maps else 0))
 
 
 def cpu_baseline(stack_h, tex_h, calib, budget_s):
@@ -100,31 +103,38 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
-    H, W, Wp, Hp, rows, vdef = CONFIGS[a.config]
-    V = a.views or vdef
+    cfg = CONFIGS[a.config]
+    H, W, Wp, Hp, rows, maps = cfg["H"], cfg["W"], cfg["Wp"], cfg["Hp"], cfg["rows"], cfg["maps"]
+    V = a.views or cfg["views"]
     rig = synth.Rig(H=H, W=W, Wp=Wp, Hp=Hp)
     calib = synth.make_calibration(rig, with_Nc=False)
     cfg_idx = int(a.config[1:])
-    stacks, texes = [], []
+    stack = None
+    tex = torch.empty((V, H, W, 3), dtype=torch.uint8, device=dev)
+    poses = torch.empty((V, 4, 4), dtype=torch.float64, device=dev) if cfg["pose"] else None
     for v in range(V):
-        gv = rank * V + v
+        gv = rank * V + v  # global view index: views sharded in contiguous blocks
         s, t = synth.render_stack(rig, seed=1000 * cfg_idx + gv, include_rows=rows,
-                                  view_deg=10.0 * gv, device=dev)
-        stacks.append(s)
-        texes.append(t)
-    stack = torch.stack(stacks) if V > 1 else stacks[0][None]
-    tex = torch.stack(texes) if V > 1 else texes[0][None]
-    del stacks, texes
+                                  view_deg=cfg["deg"] * gv, device=dev)
+        if stack is None:
+            stack = torch.empty((V,) + tuple(s.shape), dtype=torch.uint8, device=dev)
+        stack[v].copy_(s)
+        tex[v].copy_(t)
+        if poses is not None:
+            poses[v].copy_(torch.from_numpy(synth.turntable_pose(cfg["deg"] * gv)))
+        del s, t
     n_planes = stack.shape[1]
+    nc = synth.n_bits(Wp)
+    read_planes = n_planes if maps else 2 + 2 * nc
     eng = core.Reconstructor(dev)
     eng.set_calibration(calib, H, W)
     eng.reserve(V, H * W)
     n_cols, n_rows = Wp, (Hp if rows else 1080)
     out = {}
 
-    def step(o, maps=True):
+    def step(o, maps=maps):
         return eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
-                                      xyz_dtype=torch.float32, out=o)
+                                      xyz_dtype=torch.float32, poses=poses, out=o)
 
     for _ in range(a.warmup):
         step(out)
@@ -154,16 +164,19 @@ def main():
     decode_ms, count_ms, cloud_ms, nl = eng.profile_read()
     eng.sync()
 
-    # secondary: cloud-only mode (what generate_cloud runs: row planes unread)
-    out2 = {}
-    for _ in range(2):
-        step(out2, maps=False)
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    for _ in range(a.steps):
-        step(out2, maps=False)
-    torch.cuda.synchronize(dev)
-    el_cloud = time.perf_counter() - t1
+    # secondary (maps configs): cloud-only mode (what generate_cloud runs: row planes unread)
+    el_cloud = None
+    if maps:
+        out2 = {}
+        for _ in range(2):
+            step(out2, maps=False)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(a.steps):
+            step(out2, maps=False)
+        torch.cuda.synchronize(dev)
+        el_cloud = time.perf_counter() - t1
+        del out2
 
     gather_ms = None
     if world > 1:
@@ -181,9 +194,9 @@ def main():
         px_step = V * H * W
         value = world * px_step * a.steps / el
         dec_avg_ms = decode_ms / max(nl, 1)
-        ab = decode_bytes(H, W, n_planes, maps=True) * V
+        ab = decode_bytes(H, W, read_planes, maps) * V
         achieved = ab / (dec_avg_ms * 1e-3) / 1e9
-        path_b = path_bytes(H, W, n_planes, n_pts / V, maps=True) * V
+        path_b = path_bytes(H, W, read_planes, n_pts / V, maps) * V
         traffic = None
         if os.path.exists(a.traffic):
             try:
@@ -214,22 +227,24 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": f"BASELINE config {cfg_idx}: {V} x {W}x{H} view(s) per GPU per step, "
-                                   f"{n_planes} planes (Gray {'11+11' if rows else str(n_planes // 2 - 1) + '+0'}"
-                                   f" bits + inverses), outputs col/row/mask maps + fp32 xyz/BGR cloud",
+                                   f"{n_planes}-plane stacks (Gray {nc}+{n_planes // 2 - 1 - nc} bits + inverses), "
+                                   + ("col/row/mask maps + " if maps else "")
+                                   + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
                        "views_per_gpu": V, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
                        "parallelism": f"views sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_decode", "kernel_avg_ms": dec_avg_ms,
                          "algorithmic_bytes_per_launch": ab,
-                         "bytes_note": "stack planes read + col/row int32 maps written, per launch (records are overhead)"},
+                         "bytes_note": f"{read_planes} stack planes read" + (" + col/row int32 maps written" if maps else "")
+                                       + f", per launch over {V} view(s) (records are overhead)"},
             "path": {"algorithmic_bytes_per_step": path_b,
                      "GBps": path_b / (el / a.steps) / 1e9,
                      "kernel_avg_ms": {"k_decode": dec_avg_ms, "k_count": count_ms / max(nl, 1),
                                        "k_cloud": cloud_ms / max(nl, 1)}},
             "cpu_baseline": cpu,
             "points_per_view": n_pts / V,
-            "cloud_only_px_per_s": world * px_step * a.steps / el_cloud,
+            "cloud_only_px_per_s": None if el_cloud is None else world * px_step * a.steps / el_cloud,
             "gather_ms": gather_ms,
         }
         print(json.dumps(res))

@@ -226,6 +226,14 @@ __device__ __forceinline__ long long wave_sum64(long long s) {
   return s;
 }
 
+// A wave-uniform 64-bit value moved to SGPRs (so that addresses built from it
+// use scalar bases).
+__device__ __forceinline__ long long uniform64(long long v) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(v));
+  const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(static_cast<unsigned long long>(v) >> 32));
+  return static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo);
+}
+
 __device__ __forceinline__ int wave_sum(int s) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
@@ -360,7 +368,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(Params p) {
   __shared__ int s_max[kWaves];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wid = tid >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
   const int civ = blockIdx.x * kWaves + wid;  // chunk in view
   const bool live = civ < p.cpv;
@@ -580,7 +588,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(Params p) {
 // and plane gathers of nearby columns.  Every load is issued before any is
 // used (clamped, unconditional addresses).
 template <int VEC>
-__device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view, int civ, int lane) {
+__device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view, int civ, int lane, bool live) {
   const int mode = p.mode;
   const bool vec = VEC > 0;
   const int64_t HW = p.HW;
@@ -636,6 +644,8 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
         mk[s] |= (px + e < HW && p.in_mask[view * HW + px + e] != 0) ? (1u << e) : 0u;
     }
   }
+
+  if (!live) return 0;
 
   // ---- thresholds (while the loads above are in flight) ----
   int thr_w = 40, thr_c = 10;  // fixed: multi_point_cloud_process.py:36-38
@@ -702,9 +712,10 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
     us[s] = u;
     vs[s] = v;
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      pf[s][e] = (p.dbg & 128) ? make_float4(0.5f, 0.1f, 0.8f, 0.f)
-                               : p.planes32[(rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu];
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t c = (rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu;
+      pf[s][e] = p.planes32[c];
+    }
     if (!nc) {
       if (vec) {
         const float4 x4 = *reinterpret_cast<const float4*>(p.xn32 + us[s]);
@@ -797,11 +808,11 @@ template <int VEC>
 __global__ __launch_bounds__(kThreads, SLGPU_COUNT_WAVES) void k_count(Params p) {
   __shared__ int s_sum[kWaves];
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
   const int civ = blockIdx.x * kWaves + wid;
   const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
-  const int total = civ < p.cpv ? count_chunk<VEC>(p, gc, view, civ, lane) : 0;
+  const int total = count_chunk<VEC>(p, gc, view, civ, lane, civ < p.cpv);
   if (!(p.mode & M_CODES)) return;  // uniform: no barrier below
   if (lane == 0) s_sum[wid] = total;
   __syncthreads();
@@ -947,7 +958,7 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
       const uint32_t e = s_ent[j];
       bgr[i] = s_bgr[j];
       const int local = static_cast<int>(e & 1023u);
-      const int c = static_cast<int>(e >> 10);
+      const unsigned c = e >> 10;
       if (dbg & 4) {
         ra[i] = 0.25 + local;
         rb[i] = 0.5;
@@ -966,8 +977,8 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
           uu -= W;
           ++vv;
         }
-        ra[i] = p.xn[uu];
-        rb[i] = p.yn[vv];
+        ra[i] = p.xn[static_cast<unsigned>(uu)];
+        rb[i] = p.yn[static_cast<unsigned>(vv)];
       }
       pl[i] = p.planes[c];
     }
@@ -1040,19 +1051,19 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
     for (int i = 0; i < kPipe; ++i) {
       const int j = j0 + 64 * i + lane;
       if (j < total) {
-        const long long o = base + j;
+        const unsigned o = static_cast<unsigned>(j);  // offset from the chunk's first point
         if (f64out) {
-          double* xyz = static_cast<double*>(p.xyz) + 3 * o;
+          double* xyz = static_cast<double*>(p.xyz) + 3 * base + 3 * o;
           xyz[0] = X[i];
           xyz[1] = Y[i];
           xyz[2] = Z[i];
         } else {
-          float* xyz = static_cast<float*>(p.xyz) + 3 * o;
+          float* xyz = static_cast<float*>(p.xyz) + 3 * base + 3 * o;
           xyz[0] = static_cast<float>(X[i]);
           xyz[1] = static_cast<float>(Y[i]);
           xyz[2] = static_cast<float>(Z[i]);
         }
-        uint8_t* cc = p.bgr + 3 * o;
+        uint8_t* cc = p.bgr + 3 * base + 3 * o;
         cc[0] = static_cast<uint8_t>(bgr[i]);
         cc[1] = static_cast<uint8_t>(bgr[i] >> 8);
         cc[2] = static_cast<uint8_t>(bgr[i] >> 16);
@@ -1076,7 +1087,7 @@ __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
   __shared__ long long s_wred[kWaves];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wid = tid >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
   const int civ = blockIdx.x * kWaves + wid;
   const int64_t b = static_cast<int64_t>(view) * gridDim.x + blockIdx.x;  // block index in the launch
@@ -1098,6 +1109,7 @@ __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) base += s_wred[w];
   base += wave_sum(before);
+  base = uniform64(base);
   if (civ >= p.cpv) return;
   if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1)
     p.view_offsets[p.n_views] = base + p.chunk_counts[gc];
@@ -1139,6 +1151,7 @@ struct sl_ctx {
   int dbg = 0;
   // optional per-call HIP-event timing of k_decode / k_count / k_cloud
   std::vector<hipEvent_t> prof_ev;  // kProfEv events per call slot
+  std::vector<int> prof_groups;     // launch groups recorded per call
   int prof_n = 0;
 };
 
@@ -1194,7 +1207,8 @@ int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes) {
 }
 
 using KernelFn = void (*)(Params);
-constexpr int kProfEv = 4;  // events per call: before k_decode, k_count, k_cloud, after
+constexpr int kProfGroups = 64;            // launch groups timed per call (at most)
+constexpr int kProfEv = 4 * kProfGroups;   // events per call: per group before k_decode, k_count, k_cloud, after
 
 // k_decode specialisations for the benchmark configurations; everything else
 // (other bit counts, unaligned frames) runs the generic instantiation.
@@ -1237,8 +1251,10 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
   hipEvent_t* ev = nullptr;
   if (!c->prof_ev.empty() && kProfEv * (c->prof_n + 1) <= static_cast<int>(c->prof_ev.size()))
     ev = &c->prof_ev[kProfEv * c->prof_n++];
-  if (ev) HIP_TRY(c, hipEventRecord(ev[0], s));
-  for (int v0 = 0; v0 < p0.n_views; v0 += vpg) {
+  int g = 0;  // launch group index
+  for (int v0 = 0; v0 < p0.n_views; v0 += vpg, ++g) {
+    hipEvent_t* gev = (ev && g < kProfGroups) ? ev + 4 * g : nullptr;
+    if (gev) HIP_TRY(c, hipEventRecord(gev[0], s));
     const int nv = std::min(vpg, p0.n_views - v0);
     Params p = p0;
     p.n_views = nv;
@@ -1275,22 +1291,23 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       KernelFn fn = pick_decode(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode, vec);
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(kThreads), args, 0, s));
     }
-    if (ev && v0 == 0) HIP_TRY(c, hipEventRecord(ev[1], s));
+    if (gev) HIP_TRY(c, hipEventRecord(gev[1], s));
     {
       p.mode = count_mode;
       void* args[] = {&p};
       const void* fn = vec ? reinterpret_cast<const void*>(k_count<1>) : reinterpret_cast<const void*>(k_count<0>);
       HIP_TRY(c, hipLaunchKernel(fn, grid, dim3(kThreads), args, 0, s));
     }
-    if (ev && v0 == 0) HIP_TRY(c, hipEventRecord(ev[2], s));
+    if (gev) HIP_TRY(c, hipEventRecord(gev[2], s));
     if (cloud_mode >= 0) {
       p.mode = cloud_mode;
       void* args[] = {&p};
       KernelFn fn = pick_cloud(cloud_mode, vec);
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(kThreads), args, 0, s));
     }
+    if (gev) HIP_TRY(c, hipEventRecord(gev[3], s));
   }
-  if (ev) HIP_TRY(c, hipEventRecord(ev[3], s));
+  if (ev) c->prof_groups.push_back(std::min(g, kProfGroups));
   return SL_OK;
 }
 
@@ -1543,6 +1560,7 @@ int sl_profile_enable(sl_ctx* c, int max_calls) {
   HIP_TRY(c, hipSetDevice(c->device));
   for (hipEvent_t e : c->prof_ev) HIP_TRY(c, hipEventDestroy(e));
   c->prof_ev.clear();
+  c->prof_groups.clear();
   c->prof_n = 0;
   for (int i = 0; i < kProfEv * max_calls; ++i) {
     hipEvent_t e;
@@ -1557,14 +1575,18 @@ int sl_profile_read(sl_ctx* c, double* decode_ms, double* count_ms, double* clou
   HIP_TRY(c, hipSetDevice(c->device));
   double t[3] = {0.0, 0.0, 0.0};
   for (int i = 0; i < c->prof_n; ++i) {
-    hipEvent_t* ev = &c->prof_ev[kProfEv * i];
-    HIP_TRY(c, hipEventSynchronize(ev[kProfEv - 1]));
-    for (int k = 0; k < 3; ++k) {
-      float ms = 0.f;
-      HIP_TRY(c, hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
-      t[k] += ms;
+    const int ng = i < static_cast<int>(c->prof_groups.size()) ? c->prof_groups[i] : 0;
+    for (int g = 0; g < ng; ++g) {
+      hipEvent_t* ev = &c->prof_ev[kProfEv * i + 4 * g];
+      HIP_TRY(c, hipEventSynchronize(ev[3]));
+      for (int k = 0; k < 3; ++k) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+        t[k] += ms;
+      }
     }
   }
+  c->prof_groups.clear();
   if (decode_ms) *decode_ms = t[0];
   if (count_ms) *count_ms = t[1];
   if (cloud_ms) *cloud_ms = t[2];

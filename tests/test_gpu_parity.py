@@ -224,3 +224,45 @@ def test_repeat_calls_are_stable(eng):
         assert off[-1] == len(P)
         _assert_f32(xyz, P)
         np.testing.assert_array_equal(bgr, C)
+
+
+def test_launch_groups_and_view_offsets(eng):
+    """A batch larger than one launch group (16K chunks): 9 views of 1920x1080
+    are 18225 chunks -> two groups whose points chain through view_offsets.
+    Views on both sides of the group boundary bit-exact vs the oracle."""
+    from structured_light_for_3d_model_replication_amd import synth
+    V, H, W = 9, 1080, 1920
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    stacks, texes = [], []
+    for v in range(V):
+        s, t = synth.render_stack(rig, seed=300 + v, view_deg=40.0 * v, device="cuda")
+        stacks.append(s)
+        texes.append(t)
+    eng.set_calibration(cal, H, W)
+    res = eng.decode_triangulate(torch.stack(stacks), texture=torch.stack(texes), maps=False, cloud=True,
+                                 xyz_dtype=torch.float32)
+    eng.sync()
+    xyz, bgr, off = _cloud_np(res["cloud"])
+    for v in (0, 7, 8):  # first view, last view of group 0, the view of group 1
+        sth, texh = stacks[v].cpu().numpy(), texes[v].cpu().numpy()
+        _, _, _, P, C = o.decode_triangulate(list(sth), texh, cal)
+        assert off[v + 1] - off[v] == len(P)
+        _assert_f32(xyz[off[v]:off[v + 1]], P)
+        np.testing.assert_array_equal(bgr[off[v]:off[v + 1]], C)
+    assert np.all(np.diff(off) > 0)
+
+
+def test_wide_projector_13bit(eng):
+    """A 5000-column projector
+    (13-bit codes, 15-bit records, the generic decode kernel)."""
+    rig, st, tex, cal = _render(160, 256, 5000, 1080, seed=17)
+    sth, texh = st.cpu().numpy(), tex.cpu().numpy()
+    col, row, mask, P, C = o.decode_triangulate(list(sth), texh, cal, 5000, 1080)
+    res = _run(eng, sth, texh, cal, 5000, 1080, xyz_dtype=torch.float64)
+    np.testing.assert_array_equal(res["col_map"][0].cpu().numpy(), col)
+    np.testing.assert_array_equal(res["mask"][0].cpu().numpy(), mask)
+    xyz, bgr, off = _cloud_np(res["cloud"])
+    assert off[-1] == len(P)
+    np.testing.assert_array_equal(xyz.view(np.uint64), P.view(np.uint64))
+    np.testing.assert_array_equal(bgr, C)
