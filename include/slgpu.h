@@ -42,6 +42,7 @@ extern "C" {
 #define SL_ENOCALIB (-4)  /* sl_set_calib not called / shape mismatch -> ValueError       */
 #define SL_ETIMEOUT (-5)  /* reserved (no device-side waits in this version)             */
 #define SL_ECAPACITY (-6) /* output capacity smaller than the pixel count -> ValueError   */
+#define SL_EIO (-7)       /* file could not be written -> OSError                        */
 
 /* mask_mode */
 #define SL_MASK_ADAPTIVE 0 /* white > 1.5*pct95(black) & contrast > 0.05*max(contrast):
@@ -142,6 +143,18 @@ int sl_profile_enable(sl_ctx* ctx, int max_calls);
 /* Blocking: summed event time (ms) of k_decode, k_count and k_cloud over the
  * recorded calls since the last read, and their count; restarts recording. */
 int sl_profile_read(sl_ctx* ctx, double* decode_ms, double* count_ms, double* cloud_ms, int* calls);
+
+/* ASCII PLY of a cloud exactly as the reference writes it (sl_system.py:665-691,
+ * multi_point_cloud_process.py:121-131): header, then per point
+ * "%.4f %.4f %.4f %d %d %d\n" of x, y, z and the colour swapped from BGR to
+ * RGB; %.4f correctly rounded, ties to even (what Python's f"{x:.4f}" prints).
+ * Host memory, host code (no device needed); formatted on `threads` threads.
+ * xyz is n x 3 f32 or f64 (xyz_dtype), bgr n x 3 uint8.
+ * sl_format_ply: with out == NULL only *out_len is set (the byte size). */
+int sl_format_ply(const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n, int threads, char* out,
+                  int64_t out_capacity, int64_t* out_len);
+/* Write that text to `path` (replaces save_ply, sl_system.py:665-691). */
+int sl_write_ply(const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n, int threads);
 
 #ifdef __cplusplus
 }

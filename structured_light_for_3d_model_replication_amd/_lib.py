@@ -21,6 +21,7 @@ SL_EHIP = -3
 SL_ENOCALIB = -4
 SL_ETIMEOUT = -5
 SL_ECAPACITY = -6
+SL_EIO = -7
 
 SL_MASK_ADAPTIVE = 0
 SL_MASK_FIXED = 1
@@ -30,7 +31,7 @@ SL_XYZ_F64 = 1
 # every symbol include/slgpu.h declares
 EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_error", "sl_ctx_reserve",
            "sl_set_calib", "sl_decode_triangulate", "sl_triangulate_maps", "sl_sync",
-           "sl_last_thresholds", "sl_profile_enable", "sl_profile_read")
+           "sl_last_thresholds", "sl_profile_enable", "sl_profile_read", "sl_format_ply", "sl_write_ply")
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -52,6 +53,8 @@ _SIGS = {
     "sl_profile_enable": (_i32, [_vp, _i32]),
     "sl_profile_read": (_i32, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]),
+    "sl_format_ply": (_i32, [_vp, _i32, _vp, _i64, _i32, _vp, _i64, ctypes.POINTER(_i64)]),
+    "sl_write_ply": (_i32, [ctypes.c_char_p, _vp, _i32, _vp, _i64, _i32]),
 }
 
 _lock = threading.Lock()
@@ -91,4 +94,6 @@ def check(code: int, ctx=None, what: str = "") -> None:
         raise ValueError(msg)
     if code == SL_EINDEX:
         raise IndexError(msg)
+    if code == SL_EIO:
+        raise OSError(msg)
     raise SLError(f"libslgpu error {code}: {msg}")

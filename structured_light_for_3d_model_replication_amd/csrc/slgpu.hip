@@ -36,9 +36,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <stdio.h>
+
 #include <algorithm>
 #include <initializer_list>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "slgpu.h"
@@ -355,8 +358,11 @@ __device__ __forceinline__ bool has_point(const Params& p, int mode, const float
 //            banks, added to the view's global histogram once per workgroup.
 // Grid (chunk groups, views); waves past the view's last chunk run empty (the
 // workgroup barriers count them).
+#ifndef SLGPU_DECODE_WAVES
+#define SLGPU_DECODE_WAVES 1
+#endif
 template <int KC, int KR, int MODE, int VEC>
-__global__ __launch_bounds__(kThreads) void k_decode(Params p) {
+__global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params p) {
   const int mode = MODE >= 0 ? MODE : p.mode;
   const int kc = KC >= 0 ? KC : p.kc;
   const int krr = (mode & M_ROWS) ? (KR >= 0 ? KR : p.kr) : 0;
@@ -1313,6 +1319,119 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
 
 }  // namespace
 
+// ------------------------------------------------------------- PLY writer ----
+// The ASCII PLY of sl_system.py:665-691 (== multi_point_cloud_process.py:
+// 121-131): header, then per point f"{x:.4f} {y:.4f} {z:.4f} {r} {g} {b}\n"
+// with the colour swapped from BGR.  Python formats %.4f correctly rounded
+// (round-half-even on exact ties); so does fmt4 below: N = round(x * 10^4)
+// computed exactly in 128-bit integers from x's binary significand, printed
+// with 4 decimals.  Values beyond 2^53 / 10^4 and non-finite ones go through
+// glibc's snprintf("%.4f"), which is also correctly rounded ("nan", "inf"
+// as Python prints them).
+namespace {
+
+char* fmt4(char* o, double x) {
+  uint64_t bits;
+  memcpy(&bits, &x, 8);
+  const bool neg = bits >> 63;
+  const int be = static_cast<int>((bits >> 52) & 0x7ff);
+  const uint64_t frac = bits & ((1ull << 52) - 1);
+  if (be == 0x7ff || fabs(x) >= 9.0e11) {  // non-finite or large: libc
+    if (be == 0x7ff && frac) return o + sprintf(o, "nan");
+    if (be == 0x7ff) return o + sprintf(o, neg ? "-inf" : "inf");
+    return o + sprintf(o, "%.4f", x);
+  }
+  // x = m * 2^e exactly
+  const uint64_t m = be ? (frac | (1ull << 52)) : frac;
+  const int e = (be ? be : 1) - 1075;
+  unsigned __int128 v = static_cast<unsigned __int128>(m) * 10000u;
+  uint64_t N;
+  if (e >= 0) {
+    N = static_cast<uint64_t>(v << e);
+  } else if (-e >= 120) {
+    N = 0;  // |x| * 10^4 < 2^67 * 2^-120: far below 1/2
+  } else {
+    const int sh = -e;
+    const unsigned __int128 q = v >> sh;
+    const unsigned __int128 r = v - (q << sh);
+    const unsigned __int128 half = static_cast<unsigned __int128>(1) << (sh - 1);
+    N = static_cast<uint64_t>(q);
+    if (r > half || (r == half && (N & 1u))) ++N;  // round half to even
+  }
+  if (neg) *o++ = '-';
+  const uint64_t ip = N / 10000u, fp = N % 10000u;
+  char t[24];
+  int k = 0;
+  uint64_t a = ip;
+  do {
+    t[k++] = static_cast<char>('0' + a % 10u);
+    a /= 10u;
+  } while (a);
+  while (k) *o++ = t[--k];
+  *o++ = '.';
+  o[0] = static_cast<char>('0' + fp / 1000u);
+  o[1] = static_cast<char>('0' + fp / 100u % 10u);
+  o[2] = static_cast<char>('0' + fp / 10u % 10u);
+  o[3] = static_cast<char>('0' + fp % 10u);
+  return o + 4;
+}
+
+char* fmt_u8(char* o, unsigned v) {
+  if (v >= 100) *o++ = static_cast<char>('0' + v / 100u);
+  if (v >= 10) *o++ = static_cast<char>('0' + v / 10u % 10u);
+  *o++ = static_cast<char>('0' + v % 10u);
+  return o;
+}
+
+bool ply_args_ok(const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n) {
+  return n >= 0 && (n == 0 || (xyz && bgr)) && (xyz_dtype == SL_XYZ_F32 || xyz_dtype == SL_XYZ_F64);
+}
+
+// Header + the point lines in `threads` contiguous parts (formatted in parallel).
+void ply_format(const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n, int threads, std::string& head,
+                std::vector<std::vector<char>>& parts) {
+  char hb[256];
+  snprintf(hb, sizeof(hb),
+           "ply\nformat ascii 1.0\nelement vertex %lld\nproperty float x\nproperty float y\n"
+           "property float z\nproperty uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n",
+           static_cast<long long>(n));
+  head = hb;
+  const int T = static_cast<int>(
+      std::max<int64_t>(1, std::min<int64_t>(threads > 0 ? threads : 1, (n + 65535) / 65536)));
+  parts.assign(T, {});
+  constexpr size_t kLineMax = 3 * 330 + 16;  // worst case: three %.4f of ~1.8e308 + colours
+  auto work = [&](int t) {
+    const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+    std::vector<char>& b = parts[t];
+    b.resize(static_cast<size_t>(hi - lo) * 64 + kLineMax);
+    size_t used = 0;
+    for (int64_t i = lo; i < hi; ++i) {
+      if (used + kLineMax > b.size()) b.resize(b.size() * 2);
+      char* o = b.data() + used;
+      for (int k = 0; k < 3; ++k) {
+        const double v = xyz_dtype == SL_XYZ_F64 ? static_cast<const double*>(xyz)[3 * i + k]
+                                                 : static_cast<double>(static_cast<const float*>(xyz)[3 * i + k]);
+        o = fmt4(o, v);
+        *o++ = ' ';
+      }
+      o = fmt_u8(o, bgr[3 * i + 2]);
+      *o++ = ' ';
+      o = fmt_u8(o, bgr[3 * i + 1]);
+      *o++ = ' ';
+      o = fmt_u8(o, bgr[3 * i]);
+      *o++ = '\n';
+      used = static_cast<size_t>(o - b.data());
+    }
+    b.resize(used);
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
 extern "C" {
 
 int sl_abi_version(void) { return SL_ABI_VERSION; }
@@ -1607,6 +1726,40 @@ int sl_last_thresholds(sl_ctx* c, int view, float* nf, float* dr, int* thr_w, in
   if (thr_w) *thr_w = s.thr_white;
   if (thr_c) *thr_c = s.thr_contrast;
   return SL_OK;
+}
+
+int sl_format_ply(const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n, int threads, char* out,
+                  int64_t out_capacity, int64_t* out_len) {
+  if (!out_len || !ply_args_ok(xyz, xyz_dtype, bgr, n)) return SL_EINVAL;
+  std::string head;
+  std::vector<std::vector<char>> parts;
+  ply_format(xyz, xyz_dtype, bgr, n, threads, head, parts);
+  int64_t len = static_cast<int64_t>(head.size());
+  for (auto& pp : parts) len += static_cast<int64_t>(pp.size());
+  *out_len = len;
+  if (!out) return SL_OK;  // size query
+  if (out_capacity < len) return SL_ECAPACITY;
+  memcpy(out, head.data(), head.size());
+  int64_t off = static_cast<int64_t>(head.size());
+  for (auto& pp : parts) {
+    if (!pp.empty()) memcpy(out + off, pp.data(), pp.size());
+    off += static_cast<int64_t>(pp.size());
+  }
+  return SL_OK;
+}
+
+int sl_write_ply(const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n, int threads) {
+  if (!path || !ply_args_ok(xyz, xyz_dtype, bgr, n)) return SL_EINVAL;
+  std::string head;
+  std::vector<std::vector<char>> parts;
+  ply_format(xyz, xyz_dtype, bgr, n, threads, head, parts);
+  FILE* f = fopen(path, "wb");
+  if (!f) return SL_EIO;
+  bool ok = fwrite(head.data(), 1, head.size(), f) == head.size();
+  for (auto& pp : parts)
+    if (ok && !pp.empty()) ok = fwrite(pp.data(), 1, pp.size(), f) == pp.size();
+  ok = (fclose(f) == 0) && ok;
+  return ok ? SL_OK : SL_EIO;
 }
 
 }  // extern "C"

@@ -4,47 +4,54 @@ Format of server/sl_system.py:671-691 (== multi_point_cloud_process.py:121-131,
 Old/process_cloud.py:200-219): ASCII header, then per point
 ``"%.4f %.4f %.4f %d %d %d\\n"`` with the colour swapped from BGR to RGB.
 
-The reference formats one point per Python f-string (~0.3 Mpt/s).  Here whole
-chunks are formatted with one ``%`` operation on a flat tuple; ``%.4f`` and
-``f"{x:.4f}"`` both use CPython's correctly rounded ``PyOS_double_to_string``,
-so the bytes are identical.
+The reference formats one point per Python f-string (~0.3 Mpt/s).  Here the
+text is produced by libslgpu's host formatter (``sl_format_ply`` /
+``sl_write_ply``): correctly rounded %.4f (ties to even, as CPython's
+``PyOS_double_to_string``) from exact 128-bit integer arithmetic, on several
+threads.  ``tests/test_ply_io.py`` pins the bytes against the reference's own
+PLY output and against CPython's formatting on edge values.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import numpy as np
 
-_HEADER = ("ply\nformat ascii 1.0\nelement vertex {n}\nproperty float x\nproperty float y\n"
-           "property float z\nproperty uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n")
-_CHUNK = 1 << 16
+from . import _lib
+
+_THREADS = max(1, min(16, os.cpu_count() or 1))
 
 
-def ply_chunks(points, colors):
-    """Yield the PLY text in pieces (header first)."""
-    points = np.asarray(points, dtype=np.float64)
-    colors = np.asarray(colors)
-    n = len(points)
-    if len(colors) != n:
+def _arrays(points, colors):
+    P = np.asarray(points)
+    if P.dtype not in (np.float32, np.float64):
+        P = P.astype(np.float64)
+    P = np.ascontiguousarray(P)
+    C = np.ascontiguousarray(np.asarray(colors, dtype=np.uint8))
+    n = len(P)
+    if len(C) != n:
         raise ValueError("points and colors differ in length")
-    yield _HEADER.format(n=n)
-    line = "%.4f %.4f %.4f %d %d %d\n"
-    for s in range(0, n, _CHUNK):
-        p = points[s:s + _CHUNK]
-        c = colors[s:s + _CHUNK].astype(np.int64)
-        m = len(p)
-        flat = np.empty((m, 6), dtype=object)
-        flat[:, 0:3] = p.tolist() if m else np.empty((0, 3))
-        flat[:, 3] = c[:, 2].tolist()
-        flat[:, 4] = c[:, 1].tolist()
-        flat[:, 5] = c[:, 0].tolist()
-        yield (line * m) % tuple(flat.ravel().tolist())
+    if n and (P.shape[1:] != (3,) or C.shape[1:] != (3,)):
+        raise ValueError("points and colors must be (N, 3)")
+    return P, C, n, (_lib.SL_XYZ_F32 if P.dtype == np.float32 else _lib.SL_XYZ_F64)
 
 
 def ply_text(points, colors) -> str:
-    return "".join(ply_chunks(points, colors))
+    """The PLY file content as a str."""
+    P, C, n, dt = _arrays(points, colors)
+    L = _lib.load()
+    ln = ctypes.c_int64()
+    _lib.check(L.sl_format_ply(P.ctypes.data, dt, C.ctypes.data, n, _THREADS, None, 0, ctypes.byref(ln)),
+               None, "sl_format_ply")
+    buf = ctypes.create_string_buffer(ln.value)
+    _lib.check(L.sl_format_ply(P.ctypes.data, dt, C.ctypes.data, n, _THREADS, buf, ln.value, ctypes.byref(ln)),
+               None, "sl_format_ply")
+    return buf.raw[: ln.value].decode("ascii")
 
 
 def save_ply(points, colors, filename) -> None:
     """save_ply(points, colors, filename) of multi_point_cloud_process.py:121."""
-    with open(filename, "w") as f:
-        for piece in ply_chunks(points, colors):
-            f.write(piece)
+    P, C, n, dt = _arrays(points, colors)
+    _lib.check(_lib.load().sl_write_ply(os.fsencode(filename), P.ctypes.data, dt, C.ctypes.data, n, _THREADS),
+               None, f"cannot write {filename}")

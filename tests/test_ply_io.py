@@ -53,3 +53,44 @@ def test_colour_conversion_matches_opencv_weights(tmp_path):
     r, gch, b = rgb[..., 0].astype(int), rgb[..., 1].astype(int), rgb[..., 2].astype(int)
     np.testing.assert_array_equal(gray, (1868 * b + 9617 * gch + 4899 * r + 8192) >> 14)
     np.testing.assert_array_equal(io.imread_bgr(str(tmp_path / "c.png")), rgb[:, :, ::-1])
+
+
+def _python_ply(P, C):
+    """The reference's own formatting loop (sl_system.py:685-691), as text."""
+    head = ("ply\nformat ascii 1.0\nelement vertex {}\nproperty float x\nproperty float y\nproperty float z\n"
+            "property uchar red\nproperty uchar green\nproperty uchar blue\nend_header\n").format(len(P))
+    return head + "".join(f"{p[0]:.4f} {p[1]:.4f} {p[2]:.4f} {c[2]} {c[1]} {c[0]}\n"
+                          for p, c in zip(P.tolist(), np.asarray(C).tolist()))
+
+
+def test_native_formatter_matches_cpython_on_edge_values():
+    rng = np.random.default_rng(5)
+    ties = np.array([k + 0.5 for k in range(-20, 20)]) / 1e4  # not exact; plus exact binary ties below
+    # x * 10^4 exactly k + 1/2 in binary (round-half-even decides), and near-ties
+    exact_ties = np.array([1.03125, -1.03125, 1.0000305175781250, 0.0000305175781250, 3.00003125,
+                           12.34565, 0.00025, 0.00015, -0.00005, 0.0])
+    special = np.array([-0.0, 1e-320, -1e-320, 5e-324, 4.9999e-5, 5.0001e-5, -4.9999e-5, 1e15, -1e15,
+                        123456789012.3456, 9.0e11, 8.99999999999e11, 1.7976931348623157e308, -1e300,
+                        np.inf, -np.inf, np.nan, 2.0 ** 53 / 1e4, 2.0 ** 60, 0.99995, 0.99994999, 9.99995])
+    rnd = np.concatenate([rng.normal(0, 500, 20000), rng.uniform(-1, 1, 20000) * 1e-3,
+                          np.round(rng.normal(0, 100, 20000), 5), rng.normal(0, 1e8, 2000)])
+    vals = np.concatenate([ties, exact_ties, special, rnd])
+    vals = vals[: (len(vals) // 3) * 3]
+    P = vals.reshape(-1, 3)
+    C = rng.integers(0, 256, P.shape, dtype=np.uint8)
+    assert ply.ply_text(P, C) == _python_ply(P, C)
+    # float32 points are formatted as their exact float64 value (numpy upcast)
+    with np.errstate(over="ignore"):
+        P32 = P.astype(np.float32)
+    assert ply.ply_text(P32, C) == _python_ply(P32.astype(np.float64), C)
+
+
+def test_native_writer_multithreaded_large(tmp_path):
+    rng = np.random.default_rng(6)
+    P = rng.normal(0, 300, (300_000, 3))
+    C = rng.integers(0, 256, P.shape, dtype=np.uint8)
+    f = tmp_path / "big.ply"
+    ply.save_ply(P, C, str(f))
+    assert f.read_text() == _python_ply(P, C)
+    with pytest.raises(OSError):
+        ply.save_ply(P[:3], C[:3], str(tmp_path / "no_such_dir" / "x.ply"))
