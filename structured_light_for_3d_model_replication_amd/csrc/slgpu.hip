@@ -698,47 +698,47 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
   if (!codes) return 0;
 
   // ---- |n.r| > 1e-6 for the masked pixels ----
-  float4 pf[4][4];
-  float xs[4][4], ys[4];
-  int us[4], vs[4];
+  // gathers per step, two steps at a time (the scheduling barrier keeps the
+  // second pair's gathers out of the first pair's registers: 4 waves / SIMD)
   const int u_c = static_cast<int>(cpx % W), v_c = static_cast<int>(cpx / W);  // chunk origin
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    // pixel (u, v) of cpx + 256 s + 4 lane, 32-bit stepping from the origin;
-    // tail pixels past the frame are clamped to its last 4 (vec) / 1 pixel
-    int u = u_c + 256 * s + 4 * lane, v = v_c;
-    while (u >= W) {
-      u -= W;
-      ++v;
-    }
-    if (v >= p.H) {
-      v = p.H - 1;
-      u = vec ? W - 4 : W - 1;
-    }
-    us[s] = u;
-    vs[s] = v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const uint32_t c = (rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu;
-      pf[s][e] = p.planes32[c];
-    }
-    if (!nc) {
-      if (vec) {
-        const float4 x4 = *reinterpret_cast<const float4*>(p.xn32 + us[s]);
-        xs[s][0] = x4.x;
-        xs[s][1] = x4.y;
-        xs[s][2] = x4.z;
-        xs[s][3] = x4.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) xs[s][e] = p.xn32[(us[s] + e) % W];
-      }
-      ys[s] = p.yn32[vs[s]];
-    }
-  }
   int total = 0;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
+    if (s == 2) __builtin_amdgcn_sched_barrier(0);
+    float4 pf[4];
+    float xs[4], ys;
+    int us, vs;
+    {
+      // pixel (u, v) of cpx + 256 s + 4 lane, 32-bit stepping from the origin;
+      // tail pixels past the frame are clamped to its last 4 (vec) / 1 pixel
+      int u = u_c + 256 * s + 4 * lane, v = v_c;
+      while (u >= W) {
+        u -= W;
+        ++v;
+      }
+      if (v >= p.H) {
+        v = p.H - 1;
+        u = vec ? W - 4 : W - 1;
+      }
+      us = u;
+      vs = v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pf[e] = p.planes32[(rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu];
+      ys = 0.0f;
+      if (!nc) {
+        if (vec) {
+          const float4 x4 = *reinterpret_cast<const float4*>(p.xn32 + us);
+          xs[0] = x4.x;
+          xs[1] = x4.y;
+          xs[2] = x4.z;
+          xs[3] = x4.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xs[e] = p.xn32[(us + e) % W];
+        }
+        ys = p.yn32[vs];
+      }
+    }
     uint32_t nib = 0u;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -753,8 +753,8 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
         // rounding included), a > L (1.001e-6 + sum|n_i| 2^-20) implies
         // |n.r| > 1.001e-6 for the exact ray, clear of the reference's f64
         // rounding.  Pixels that fail take the bounded test below.
-        const float4 f = pf[s][e];
-        const float x = xs[s][e], y = vec ? ys[s] : 0.0f;
+        const float4 f = pf[e];
+        const float x = xs[e], y = vec ? ys : 0.0f;
         if (vec) {
           const float a = fabsf(f.x * x + f.y * y + f.z);
           const float L = fabsf(x) + fabsf(y) + 1.0f;
@@ -767,7 +767,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
       }
       {
         const int c = static_cast<int>((rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu);
-        int u = us[s] + e, v = vs[s];
+        int u = us + e, v = vs;
         if (!vec && u >= W) {
           u -= W;
           ++v;
@@ -780,12 +780,12 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
           z = static_cast<float>(p.nc_rays[2 * HW + q]);
           inv = 1.0f;
         } else {
-          x = xs[s][e];
-          y = vec ? ys[s] : p.yn32[v];
+          x = xs[e];
+          y = vec ? ys : p.yn32[v];
           z = 1.0f;
           inv = __frsqrt_rn(x * x + y * y + 1.0f);
         }
-        if (has_point(p, mode, pf[s][e], c, x, y, z, inv, u, v, q)) nib |= 1u << e;
+        if (has_point(p, mode, pf[e], c, x, y, z, inv, u, v, q)) nib |= 1u << e;
       }
     }
     total += __popc(nib);
