@@ -854,6 +854,10 @@ constexpr int kPipe = SLGPU_PIPE;  // points per lane per pass in k_cloud
 #define SLGPU_STAGE_OUT 0
 #endif
 constexpr bool kStageOut = SLGPU_STAGE_OUT != 0;  // f32 points leave through an LDS stage
+#ifndef SLGPU_LDS_BGR
+#define SLGPU_LDS_BGR 1
+#endif
+constexpr bool kLdsBgr = SLGPU_LDS_BGR != 0;  // compacted colours in LDS (else re-read from the texture)
 
 // One chunk (global index gc, output offset base) of k_cloud, by one wave.
 template <int MODE, int VEC>
@@ -935,7 +939,7 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
       }
       if ((ptbits >> k) & 1u) {
         s_ent[idx] = static_cast<uint32_t>(lane * kPx + k) | (code << 10);
-        s_bgr[idx] = bgr;
+        if (kLdsBgr) s_bgr[idx] = bgr;
       }
       idx += (ptbits >> k) & 1u;
     }
@@ -962,8 +966,15 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
     for (int i = 0; i < kPipe; ++i) {
       const int j = min(j0 + 64 * i + lane, total - 1);  // past the end: repeat the last point
       const uint32_t e = s_ent[j];
-      bgr[i] = s_bgr[j];
       const int local = static_cast<int>(e & 1023u);
+      if (kLdsBgr) {
+        bgr[i] = s_bgr[j];
+      } else if (has_tex) {
+        const uint8_t* t = p.tex + view * p.tex_vs + 3 * (cpx + local);
+        bgr[i] = t[0] | (static_cast<uint32_t>(t[1]) << 8) | (static_cast<uint32_t>(t[2]) << 16);
+      } else {
+        bgr[i] = static_cast<uint32_t>(p.stack[view * p.stack_vs + cpx + local]) * 0x010101u;
+      }
       const unsigned c = e >> 10;
       if (dbg & 4) {
         ra[i] = 0.25 + local;
@@ -1087,9 +1098,9 @@ constexpr int kPrefixBatch = 4;
 template <int MODE, int VEC>
 __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
   __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
-  __shared__ uint32_t s_bgr[kWaves][kChunk];  // their B | G << 8 | R << 16
-  __shared__ float s_sxyz[kWaves][192];       // output stage: 64 points' xyz
-  __shared__ uint8_t s_scol[kWaves][192];     // and their colour bytes
+  __shared__ uint32_t s_bgr[kWaves][kLdsBgr ? kChunk : 1];  // their B | G << 8 | R << 16
+  __shared__ float s_sxyz[kWaves][kStageOut ? 192 : 1];      // output stage: 64 points' xyz
+  __shared__ uint8_t s_scol[kWaves][kStageOut ? 192 : 4];    // and their colour bytes
   __shared__ long long s_wred[kWaves];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
