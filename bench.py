@@ -7,9 +7,12 @@
 A step is one pass of the hot path over one batch of synthetic views resident
 in HBM -- k_decode (Gray decode, Gray->binary, black-plane histogram), k_count
 (adaptive-mask thresholds, mask, point/no-point decision, chunk counts),
-k_cloud (chunk offsets, f64 ray/plane intersection, ordered stores) -- producing what the reference's
+k_cloud (chunk offsets, ray/plane intersection, ordered stores) -- producing what the reference's
 gray_decode + reconstruct_point_cloud return: col_map, row_map, mask and the
-(xyz, BGR) cloud.  Default workload = BASELINE config 2: one 3840x2160 view,
+(xyz, BGR) cloud.  xyz is float32: by default SL_XYZ_F32_FAST (f32 arithmetic,
+per-coordinate relative error <= 1.02e-5 of the reference's f64, inside the
+1e-4 of BASELINE.json; --xyz exact: the correctly rounded float32 of the f64,
+f64 arithmetic); the other mode is reported beside it ("alt_xyz_mode").  Default workload = BASELINE config 2: one 3840x2160 view,
 11+11-bit column+row Gray code with inverses (46 planes), per GPU per step.
 Multi-GPU: weak scaling, views sharded over ranks with no data-path
 collective; the RCCL gather of the clouds to rank 0 is timed separately
@@ -46,6 +49,11 @@ CONFIGS = {
 }
 
 
+XYZ_MODES = {True: "SL_XYZ_F32_FAST: f32 arithmetic, per-coordinate rel err <= 1.02e-5 of the reference's "
+                    "f64 (tolerance 1e-4); kappa > 16 points exact",
+             False: "SL_XYZ_F32: f64 arithmetic, xyz = correctly rounded float32 of the reference's f64"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -55,6 +63,9 @@ def parse():
     ap.add_argument("--views", type=int, default=None, help="views per GPU per step (default per config)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
+    ap.add_argument("--xyz", default="fast", choices=["fast", "exact"],
+                    help="fast: SL_XYZ_F32_FAST (f32 arithmetic, rel err <= 1.02e-5 of the reference's f64); "
+                         "exact: SL_XYZ_F32 (correctly rounded float32 of the reference's f64)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per k_decode launch (from profiles/)")
@@ -132,9 +143,13 @@ def main():
     n_cols, n_rows = Wp, (Hp if rows else 1080)
     out = {}
 
-    def step(o, maps=maps):
+    # SL_XYZ_F32_FAST applies without a pose (include/slgpu.h); the other
+    # xyz mode is timed as a secondary
+    head_fast = a.xyz == "fast" and poses is None
+
+    def step(o, maps=maps, fast=head_fast):
         return eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
-                                      xyz_dtype=torch.float32, poses=poses, out=o)
+                                      xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o)
 
     for _ in range(a.warmup):
         step(out)
@@ -177,6 +192,27 @@ def main():
         torch.cuda.synchronize(dev)
         el_cloud = time.perf_counter() - t1
         del out2
+
+    # secondary: the other xyz mode (fast <-> correctly rounded), same workload
+    alt = None
+    if poses is None:
+        out3 = {}
+        for _ in range(2):
+            step(out3, fast=not head_fast)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(a.steps):
+            step(out3, fast=not head_fast)
+        torch.cuda.synchronize(dev)
+        el_alt = time.perf_counter() - t1
+        eng.profile_enable(a.steps)
+        for _ in range(a.steps):
+            step(out3, fast=not head_fast)
+        _, _, acloud_ms, anl = eng.profile_read()
+        eng.sync()
+        alt = {"xyz_mode": XYZ_MODES[not head_fast], "px_per_s": world * V * H * W * a.steps / el_alt,
+               "ms_per_step": 1e3 * el_alt / a.steps, "k_cloud_ms": acloud_ms / max(anl, 1)}
+        del out3
 
     gather_ms = None
     if world > 1:
@@ -224,7 +260,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
+            "dtype": "u8+f32" if head_fast else "u8+f64",
             "data": "synthetic",
             "config": {"workload": f"BASELINE config {cfg_idx}: {V} x {W}x{H} view(s) per GPU per step, "
                                    f"{n_planes}-plane stacks (Gray {nc}+{n_planes // 2 - 1 - nc} bits + inverses), "
@@ -246,6 +282,8 @@ def main():
             "points_per_view": n_pts / V,
             "cloud_only_px_per_s": None if el_cloud is None else world * px_step * a.steps / el_cloud,
             "gather_ms": gather_ms,
+            "xyz_mode": XYZ_MODES[head_fast],
+            "alt_xyz_mode": alt,
         }
         print(json.dumps(res))
     if world > 1:

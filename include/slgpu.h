@@ -53,6 +53,11 @@ extern "C" {
 /* xyz_dtype */
 #define SL_XYZ_F32 0 /* 12 B/point, the round-to-nearest fp32 of the reference's f64   */
 #define SL_XYZ_F64 1 /* 24 B/point, bit-identical to the reference's f64              */
+/* 12 B/point, f32 arithmetic: per-coordinate relative error vs the reference's f64
+ * <= (11 + 10*16) * 2^-24 ~ 1.0e-5 (north-star tolerance 1e-4).  Points with
+ * condition number sum|n_i r_i| / |n.r| > 16 are computed exactly.  Applies when
+ * Oc = 0, no Nc table and no pose; otherwise identical to SL_XYZ_F32.          */
+#define SL_XYZ_F32_FAST 2
 
 typedef struct sl_ctx sl_ctx;
 

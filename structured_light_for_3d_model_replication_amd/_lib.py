@@ -27,6 +27,7 @@ SL_MASK_ADAPTIVE = 0
 SL_MASK_FIXED = 1
 SL_XYZ_F32 = 0
 SL_XYZ_F64 = 1
+SL_XYZ_F32_FAST = 2
 
 # every symbol include/slgpu.h declares
 EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_error", "sl_ctx_reserve",

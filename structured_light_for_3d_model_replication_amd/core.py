@@ -75,6 +75,16 @@ def calibration_arrays(calib: dict, H: int, W: int):
     return _f64c(calib["cam_K"]).reshape(3, 3), Oc, _f64c(planes[:, :4]), None if Nc is None else _f64c(Nc)
 
 
+def _xyz_code(xyz_dtype, fast_f32: bool) -> int:
+    if xyz_dtype == torch.float64:
+        if fast_f32:
+            raise ValueError("fast_f32 needs xyz_dtype=torch.float32")
+        return _lib.SL_XYZ_F64
+    if xyz_dtype != torch.float32:
+        raise ValueError("xyz_dtype must be torch.float32 or torch.float64")
+    return _lib.SL_XYZ_F32_FAST if fast_f32 else _lib.SL_XYZ_F32
+
+
 class Reconstructor:
     """Owns one device context.  Thread-safe: calls are serialised per context."""
 
@@ -135,7 +145,8 @@ class Reconstructor:
     def decode_triangulate(self, stack: torch.Tensor, n_cols: int = 1920, n_rows: int = 1080, *,
                            texture: torch.Tensor | None = None, mask_mode: str = "adaptive",
                            maps: bool = False, cloud: bool = True, xyz_dtype=torch.float32,
-                           poses: torch.Tensor | None = None, stream=None, out: dict | None = None):
+                           poses: torch.Tensor | None = None, fast_f32: bool = False, stream=None,
+                           out: dict | None = None):
         """Fused decode (+ triangulation) of a device stack.
 
         ``stack`` uint8 [n_img, H, W] or [V, n_img, H, W] on this device;
@@ -143,6 +154,9 @@ class Reconstructor:
         replicated).  Returns a dict with ``col_map``/``row_map`` int32,
         ``mask`` bool ([V,H,W], when ``maps``) and ``cloud`` (a ``Cloud``,
         when ``cloud``).  Asynchronous on ``stream``; ``out`` reuses buffers.
+        ``fast_f32`` (float32 xyz only): SL_XYZ_F32_FAST -- f32 arithmetic,
+        per-coordinate relative error <= 1.02e-5 vs the reference's f64,
+        instead of the correctly rounded float32 of it.
         """
         if stack.dtype != torch.uint8 or stack.device != self.device:
             raise ValueError("stack must be a uint8 tensor on the reconstructor's device")
@@ -175,7 +189,7 @@ class Reconstructor:
                 out["mask_u8"] = torch.empty((V, H, W), dtype=torch.uint8, device=self.device)
             row, msk = out["row_map"], out["mask_u8"]
         cap = V * H * W
-        xyz_code = _lib.SL_XYZ_F64 if xyz_dtype == torch.float64 else _lib.SL_XYZ_F32
+        xyz_code = _xyz_code(xyz_dtype, fast_f32)
         if cloud:
             xyz = out.get("xyz")
             if xyz is None or xyz.shape[0] < cap or xyz.dtype != xyz_dtype:
@@ -201,7 +215,7 @@ class Reconstructor:
         return res
 
     def triangulate_maps(self, col_map: torch.Tensor, mask: torch.Tensor, texture: torch.Tensor, *,
-                         xyz_dtype=torch.float64, poses=None, stream=None) -> Cloud:
+                         xyz_dtype=torch.float64, poses=None, fast_f32: bool = False, stream=None) -> Cloud:
         """reconstruct_point_cloud on device maps: col_map int32 [V,H,W] (or
         [H,W]), mask bool/uint8, texture uint8 BGR [V,H,W,3]."""
         if col_map.dim() == 2:
@@ -219,7 +233,7 @@ class Reconstructor:
         xyz = torch.empty((cap, 3), dtype=xyz_dtype, device=self.device)
         bgr = torch.empty((cap, 3), dtype=torch.uint8, device=self.device)
         vo = torch.empty(V + 1, dtype=torch.int64, device=self.device)
-        xyz_code = _lib.SL_XYZ_F64 if xyz_dtype == torch.float64 else _lib.SL_XYZ_F32
+        xyz_code = _xyz_code(xyz_dtype, fast_f32)
         with self._lock:
             if (self._H, self._W) != (H, W):
                 raise ValueError(f"calibration is for {self._W}x{self._H}, maps are {W}x{H}")

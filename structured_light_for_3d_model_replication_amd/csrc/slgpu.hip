@@ -107,6 +107,8 @@ constexpr int M_FROMMAPS = 8;  // input is a caller's (col_map, mask) instead of
 constexpr int M_NC = 16;       // rays from a device Nc table instead of pinhole K
 constexpr int M_ROWS = 32;     // k_decode: decode the row sequence
 constexpr int M_HIST = 64;     // adaptive mask: k_decode builds the histogram, k_count reads it
+constexpr int M_FAST32 = 128;  // k_cloud: f32 arithmetic for well-conditioned points (SL_XYZ_F32_FAST)
+constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
 
 constexpr int kSlot = 272;                 // histogram of one view: 256 bins + max + pad (u32)
 constexpr int kHistRep = 32;               // LDS histogram replicas (one per lane of a half-wave)
@@ -958,7 +960,84 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   const double* pose = p.poses ? p.poses + 16 * view : nullptr;
   const bool f64out = (mode & M_XYZ64) != 0;
   const int dbg = p.dbg;
+  auto point_bgr = [&](int j, int local) -> uint32_t {
+    if (kLdsBgr) return s_bgr[j];
+    if (has_tex) {
+      const uint8_t* t = p.tex + view * p.tex_vs + 3 * (cpx + local);
+      return t[0] | (static_cast<uint32_t>(t[1]) << 8) | (static_cast<uint32_t>(t[2]) << 16);
+    }
+    return static_cast<uint32_t>(p.stack[view * p.stack_vs + cpx + local]) * 0x010101u;
+  };
   for (int j0 = 0; j0 < total; j0 += 64 * kPipe) {
+    if (mode & M_FAST32) {
+      // SL_XYZ_F32_FAST (Oc = 0, pinhole rays, no pose; host-checked): the
+      // same formula in f32 -- rsq-normalised ray, f32 plane, rcp -- for
+      // points whose condition number kappa = sum|n_i r_i| / |n.r| is at most
+      // kFastKappa; the rest take the exact f64 route below.  Per-coordinate
+      // relative error vs the reference's f64 <= (11 + 10 kappa) 2^-24
+      // ("f32-fast").
+      float fx[kPipe], fy[kPipe];
+      float4 fp[kPipe];
+      uint32_t bgr[kPipe];
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
+        const int j = min(j0 + 64 * i + lane, total - 1);
+        const uint32_t e = s_ent[j];
+        const int local = static_cast<int>(e & 1023u);
+        bgr[i] = point_bgr(j, local);
+        int uu = u_c + local, vv = v_c;
+        while (uu >= W) {
+          uu -= W;
+          ++vv;
+        }
+        fx[i] = p.xn32[static_cast<unsigned>(uu)];
+        fy[i] = p.yn32[static_cast<unsigned>(vv)];
+        fp[i] = p.planes32[e >> 10];
+      }
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
+        const int j = j0 + 64 * i + lane;
+        const float x = fx[i], y = fy[i];
+        const float inv = __builtin_amdgcn_rsqf((x * x + y * y) + 1.0f);
+        const float r0 = x * inv, r1 = y * inv;
+        const float a0 = fp[i].x * r0, a1 = fp[i].y * r1, a2 = fp[i].z * inv;
+        const float den = (a0 + a1) + a2;
+        const float S = (fabsf(a0) + fabsf(a1)) + fabsf(a2);
+        float X, Y, Z;
+        if (S <= kFastKappa * fabsf(den)) {
+          const float t = -fp[i].w * __builtin_amdgcn_rcpf(den);
+          X = 0.0f + r0 * t;  // o + r t with o = +0: -0 becomes +0 as in f64
+          Y = 0.0f + r1 * t;
+          Z = 0.0f + inv * t;
+        } else {  // ill-conditioned: exact f64, as the path below
+          const uint32_t e = s_ent[min(j, total - 1)];
+          int uu = u_c + static_cast<int>(e & 1023u), vv = v_c;
+          while (uu >= W) {
+            uu -= W;
+            ++vv;
+          }
+          const double xd = p.xn[uu], yd = p.yn[vv];
+          const double4 pd = p.planes[e >> 10];
+          const double nrm = sqrt((xd * xd + yd * yd) + 1.0);
+          const double d0 = xd / nrm, d1 = yd / nrm, d2 = 1.0 / nrm;
+          const double td = -pd.w / ((pd.x * d0 + pd.y * d1) + pd.z * d2);
+          X = static_cast<float>(p.o0 + d0 * td);
+          Y = static_cast<float>(p.o1 + d1 * td);
+          Z = static_cast<float>(p.o2 + d2 * td);
+        }
+        if (j < total) {
+          float* xyz = static_cast<float*>(p.xyz) + 3 * base + 3 * static_cast<unsigned>(j);
+          xyz[0] = X;
+          xyz[1] = Y;
+          xyz[2] = Z;
+          uint8_t* cc = p.bgr + 3 * base + 3 * static_cast<unsigned>(j);
+          cc[0] = static_cast<uint8_t>(bgr[i]);
+          cc[1] = static_cast<uint8_t>(bgr[i] >> 8);
+          cc[2] = static_cast<uint8_t>(bgr[i] >> 16);
+        }
+      }
+      continue;
+    }
     double ra[kPipe], rb[kPipe], rcz[kPipe];  // pinhole: x, y, -; Nc: r0, r1, r2
     double4 pl[kPipe];
     uint32_t bgr[kPipe];
@@ -967,14 +1046,7 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
       const int j = min(j0 + 64 * i + lane, total - 1);  // past the end: repeat the last point
       const uint32_t e = s_ent[j];
       const int local = static_cast<int>(e & 1023u);
-      if (kLdsBgr) {
-        bgr[i] = s_bgr[j];
-      } else if (has_tex) {
-        const uint8_t* t = p.tex + view * p.tex_vs + 3 * (cpx + local);
-        bgr[i] = t[0] | (static_cast<uint32_t>(t[1]) << 8) | (static_cast<uint32_t>(t[2]) << 16);
-      } else {
-        bgr[i] = static_cast<uint32_t>(p.stack[view * p.stack_vs + cpx + local]) * 0x010101u;
-      }
+      bgr[i] = point_bgr(j, local);
       const unsigned c = e >> 10;
       if (dbg & 4) {
         ra[i] = 0.25 + local;
@@ -1246,6 +1318,7 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
 
 KernelFn pick_cloud(int mode, bool vec) {
   if (vec && mode == 0) return k_cloud<0, 1>;  // f32 xyz, pinhole rays
+  if (vec && mode == M_FAST32) return k_cloud<M_FAST32, 1>;
   return vec ? k_cloud<-1, 1> : k_cloud<-1, 0>;
 }
 
@@ -1533,7 +1606,7 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
   HIP_TRY(c, hipMemcpy(c->d_yn, yn.data(), sizeof(double) * H, hipMemcpyHostToDevice));
   {
     std::vector<float> f(4 * static_cast<size_t>(Wp) + W + H);
-    for (int i = 0; i < 4 * Wp; ++i) f[i] = static_cast<float>(planes[i]);
+    for (int i = 0; i < 4 * Wp; ++i) f[i] = static_cast<float>(pl[i]);  // w: f32 of n.Oc + d
     for (int u = 0; u < W; ++u) f[4 * Wp + u] = static_cast<float>(xn[u]);
     for (int v = 0; v < H; ++v) f[4 * Wp + W + v] = static_cast<float>(yn[v]);
     HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_f32), sizeof(float) * f.size()));
@@ -1560,11 +1633,23 @@ static int common_out_checks(sl_ctx* c, int n_views, int H, int W, void* xyz, in
   if (xyz && (H != c->H || W != c->W))
     return fail(c, SL_ENOCALIB, "frame size differs from the calibrated camera");
   if (xyz && (!bgr || !view_offsets)) return fail(c, SL_EINVAL, "xyz_out needs bgr_out and view_offsets");
-  if (xyz && (xyz_dtype != SL_XYZ_F32 && xyz_dtype != SL_XYZ_F64)) return fail(c, SL_EINVAL, "bad xyz_dtype");
+  if (xyz && (xyz_dtype != SL_XYZ_F32 && xyz_dtype != SL_XYZ_F64 && xyz_dtype != SL_XYZ_F32_FAST))
+    return fail(c, SL_EINVAL, "bad xyz_dtype");
   if (xyz && (!aligned16(xyz) || !aligned16(bgr))) return fail(c, SL_EINVAL, "xyz/bgr must be 16-byte aligned");
   if (xyz && cap < static_cast<int64_t>(n_views) * H * W)
     return fail(c, SL_ECAPACITY, "out_capacity < n_views*H*W");
   return SL_OK;
+}
+
+// k_cloud mode bits of an output dtype.  SL_XYZ_F32_FAST takes the f32 route
+// only where its error bound holds as stated: Oc = 0 (P = r t, no
+// cancellation), pinhole rays and no pose; otherwise it is SL_XYZ_F32.
+static int xyz_mode_bits(const sl_ctx* c, int xyz_dtype, const double* poses) {
+  const int nc_bit = c->d_nc ? M_NC : 0;
+  if (xyz_dtype == SL_XYZ_F64) return M_XYZ64 | nc_bit;
+  const bool fast = xyz_dtype == SL_XYZ_F32_FAST && !c->d_nc && !poses && c->Oc[0] == 0.0 &&
+                    c->Oc[1] == 0.0 && c->Oc[2] == 0.0;
+  return fast ? M_FAST32 : nc_bit;
 }
 
 static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
@@ -1641,7 +1726,7 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   const int hist_bit = mask_mode == SL_MASK_ADAPTIVE ? M_HIST : 0;
   const int decode_mode = (maps ? (M_MAPS | M_ROWS) : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit;
   const int count_mode = (maps ? M_MAPS : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit;
-  const int cloud_mode = xyz ? ((xyz_dtype == SL_XYZ_F64 ? M_XYZ64 : 0) | nc_bit) : -1;
+  const int cloud_mode = xyz ? xyz_mode_bits(c, xyz_dtype, poses) : -1;
   const bool vec = (W % 16 == 0) && W >= 64 && aligned16(stack) && (stack_vs % 16 == 0) &&
                    (!tex || (aligned16(tex) && tex_vs % 16 == 0)) &&
                    (!maps || (aligned16(col_out) && aligned16(row_out) && aligned16(mask_out)));
@@ -1671,7 +1756,7 @@ int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, 
   const int nc_bit = c->d_nc ? M_NC : 0;
   const int decode_mode = M_FROMMAPS | M_CODES | nc_bit;
   const int count_mode = M_FROMMAPS | M_CODES | nc_bit;
-  const int cloud_mode = (xyz_dtype == SL_XYZ_F64 ? M_XYZ64 : 0) | nc_bit;
+  const int cloud_mode = xyz_mode_bits(c, xyz_dtype, poses);
   const bool vec = (W % 16 == 0) && W >= 64 && aligned16(col_map) && aligned16(mask) && aligned16(tex);
   HIP_TRY(c, hipSetDevice(c->device));
   return launch(c, p, vec, decode_mode, count_mode, cloud_mode, static_cast<hipStream_t>(stream));
