@@ -1,9 +1,7 @@
-# k_cloud / k_decode ablations via SLGPU_DEBUG (measurement only); args = dbg values
-set -u
-cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
-: > gpurun_out/kbench.log
-for d in "${@:-0}"; do
-  SLGPU_DEBUG=$d timeout -k 10 120 python -u scripts/kbench.py --reps 20 >> gpurun_out/kbench.log 2>&1 || exit $?
+# kernel-bench ablations (SLGPU_DEBUG values given as args) for one kbench variant
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && : > gpurun_out/kb_ablate.log
+only=${ONLY:-maps+cloud}
+for d in "$@"; do
+  SLGPU_DEBUG=$d timeout -k 10 120 python -u scripts/kbench.py --reps 20 --only "$only" >> gpurun_out/kb_ablate.log 2>&1 || exit $?
 done
-grep -E "variant" gpurun_out/kbench.log
+grep variant gpurun_out/kb_ablate.log | grep -v torch
