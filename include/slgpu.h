@@ -161,6 +161,13 @@ int sl_format_ply(const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n,
 /* Write that text to `path` (replaces save_ply, sl_system.py:665-691). */
 int sl_write_ply(const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n, int threads);
 
+/* Binary little-endian PLY with the same header properties (float x y z,
+ * uchar red green blue; colour swapped from BGR): 15-byte records, xyz rounded
+ * to float32 when xyz_dtype is SL_XYZ_F64.  What Open3D's write_point_cloud
+ * produces by default, for the merge stage (processing.py:116-182). */
+int sl_write_ply_binary(const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n,
+                        int threads);
+
 #ifdef __cplusplus
 }
 #endif

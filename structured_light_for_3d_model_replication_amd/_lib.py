@@ -32,7 +32,8 @@ SL_XYZ_F32_FAST = 2
 # every symbol include/slgpu.h declares
 EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_error", "sl_ctx_reserve",
            "sl_set_calib", "sl_decode_triangulate", "sl_triangulate_maps", "sl_sync",
-           "sl_last_thresholds", "sl_profile_enable", "sl_profile_read", "sl_format_ply", "sl_write_ply")
+           "sl_last_thresholds", "sl_profile_enable", "sl_profile_read", "sl_format_ply", "sl_write_ply",
+           "sl_write_ply_binary")
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -56,6 +57,7 @@ _SIGS = {
                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]),
     "sl_format_ply": (_i32, [_vp, _i32, _vp, _i64, _i32, _vp, _i64, ctypes.POINTER(_i64)]),
     "sl_write_ply": (_i32, [ctypes.c_char_p, _vp, _i32, _vp, _i64, _i32]),
+    "sl_write_ply_binary": (_i32, [ctypes.c_char_p, _vp, _i32, _vp, _i64, _i32]),
 }
 
 _lock = threading.Lock()

@@ -1858,4 +1858,49 @@ int sl_write_ply(const char* path, const void* xyz, int xyz_dtype, const uint8_t
   return ok ? SL_OK : SL_EIO;
 }
 
+// Binary little-endian PLY with the reference header's properties (float
+// x y z, uchar red green blue): 15-byte records, packed on `threads` threads.
+int sl_write_ply_binary(const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n,
+                        int threads) {
+  if (!path || !ply_args_ok(xyz, xyz_dtype, bgr, n)) return SL_EINVAL;
+  char hb[256];
+  const int hl = snprintf(hb, sizeof(hb),
+                          "ply\nformat binary_little_endian 1.0\nelement vertex %lld\nproperty float x\n"
+                          "property float y\nproperty float z\nproperty uchar red\nproperty uchar green\n"
+                          "property uchar blue\nend_header\n",
+                          static_cast<long long>(n));
+  std::vector<char> body;
+  try {
+    body.resize(static_cast<size_t>(n) * 15);
+  } catch (const std::bad_alloc&) {
+    return SL_EINVAL;
+  }
+  const int T = static_cast<int>(
+      std::max<int64_t>(1, std::min<int64_t>(threads > 0 ? threads : 1, (n + 262143) / 262144)));
+  auto work = [&](int t) {
+    const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+    char* o = body.data() + 15 * lo;
+    for (int64_t i = lo; i < hi; ++i, o += 15) {
+      float v[3];
+      for (int k = 0; k < 3; ++k)
+        v[k] = xyz_dtype == SL_XYZ_F64 ? static_cast<float>(static_cast<const double*>(xyz)[3 * i + k])
+                                       : static_cast<const float*>(xyz)[3 * i + k];
+      memcpy(o, v, 12);
+      o[12] = static_cast<char>(bgr[3 * i + 2]);
+      o[13] = static_cast<char>(bgr[3 * i + 1]);
+      o[14] = static_cast<char>(bgr[3 * i]);
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  FILE* f = fopen(path, "wb");
+  if (!f) return SL_EIO;
+  bool ok = fwrite(hb, 1, static_cast<size_t>(hl), f) == static_cast<size_t>(hl);
+  if (ok && n) ok = fwrite(body.data(), 1, body.size(), f) == body.size();
+  ok = (fclose(f) == 0) && ok;
+  return ok ? SL_OK : SL_EIO;
+}
+
 }  // extern "C"

@@ -50,8 +50,63 @@ def ply_text(points, colors) -> str:
     return buf.raw[: ln.value].decode("ascii")
 
 
-def save_ply(points, colors, filename) -> None:
-    """save_ply(points, colors, filename) of multi_point_cloud_process.py:121."""
+def save_ply(points, colors, filename, binary: bool = False) -> None:
+    """save_ply(points, colors, filename) of multi_point_cloud_process.py:121.
+
+    ``binary=True`` writes binary_little_endian with the same properties
+    (float32 xyz, uchar RGB): what Open3D's write_point_cloud writes by default.
+    """
     P, C, n, dt = _arrays(points, colors)
-    _lib.check(_lib.load().sl_write_ply(os.fsencode(filename), P.ctypes.data, dt, C.ctypes.data, n, _THREADS),
-               None, f"cannot write {filename}")
+    fn = _lib.load().sl_write_ply_binary if binary else _lib.load().sl_write_ply
+    _lib.check(fn(os.fsencode(filename), P.ctypes.data, dt, C.ctypes.data, n, _THREADS), None,
+               f"cannot write {filename}")
+
+
+_PLY_TYPES = {"float": "<f4", "float32": "<f4", "double": "<f8", "float64": "<f8", "uchar": "u1",
+              "uint8": "u1", "char": "i1", "int8": "i1", "short": "<i2", "int16": "<i2", "ushort": "<u2",
+              "uint16": "<u2", "int": "<i4", "int32": "<i4", "uint": "<u4", "uint32": "<u4"}
+
+
+def read_ply(filename):
+    """-> (points float64 (N,3), colors uint8 (N,3) BGR) of a vertex-only PLY
+    (ASCII or binary_little_endian), as o3d.io.read_point_cloud feeds
+    processing.py:116-182.  Colour is swapped back to BGR, the reference's
+    in-memory order; a file without colour gives zeros."""
+    with open(filename, "rb") as f:
+        data = f.read()
+    end = data.find(b"end_header\n")
+    if not data.startswith(b"ply") or end < 0:
+        raise ValueError(f"{filename}: not a PLY file")
+    head = data[:end].decode("ascii").split("\n")
+    fmt, n, props = None, 0, []
+    for line in head:
+        t = line.split()
+        if not t:
+            continue
+        if t[0] == "format":
+            fmt = t[1]
+        elif t[0] == "element":
+            if t[1] != "vertex":
+                raise ValueError(f"{filename}: only vertex elements are supported")
+            n = int(t[2])
+        elif t[0] == "property":
+            if t[1] == "list":
+                raise ValueError(f"{filename}: list properties are not supported")
+            props.append((t[2], _PLY_TYPES[t[1]]))
+    body = data[end + len(b"end_header\n"):]
+    names = [p for p, _ in props]
+    if fmt == "ascii":
+        rows = np.loadtxt(body.decode("ascii").splitlines(), dtype=np.float64, ndmin=2) if n else \
+            np.zeros((0, len(props)))
+        cols = {p: rows[:, i] for i, p in enumerate(names)}
+    elif fmt == "binary_little_endian":
+        rec = np.frombuffer(body, dtype=np.dtype(props), count=n)
+        cols = {p: rec[p] for p in names}
+    else:
+        raise ValueError(f"{filename}: unsupported format {fmt}")
+    P = np.stack([cols["x"], cols["y"], cols["z"]], 1).astype(np.float64)
+    if all(c in cols for c in ("red", "green", "blue")):
+        C = np.stack([cols["blue"], cols["green"], cols["red"]], 1).astype(np.uint8)
+    else:
+        C = np.zeros((n, 3), np.uint8)
+    return P, C

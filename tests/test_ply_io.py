@@ -94,3 +94,39 @@ def test_native_writer_multithreaded_large(tmp_path):
     assert f.read_text() == _python_ply(P, C)
     with pytest.raises(OSError):
         ply.save_ply(P[:3], C[:3], str(tmp_path / "no_such_dir" / "x.ply"))
+
+
+def test_binary_ply_layout_and_roundtrip(tmp_path):
+    """Binary PLY: the reference header's properties as binary_little_endian,
+    15-byte records (float32 xyz, RGB); read_ply gives back (P, C BGR)."""
+    rng = np.random.default_rng(7)
+    P = rng.normal(0, 300, (200_003, 3))
+    C = rng.integers(0, 256, P.shape, dtype=np.uint8)
+    f = tmp_path / "b.ply"
+    ply.save_ply(P, C, str(f), binary=True)
+    raw = f.read_bytes()
+    head = (b"ply\nformat binary_little_endian 1.0\nelement vertex 200003\nproperty float x\n"
+            b"property float y\nproperty float z\nproperty uchar red\nproperty uchar green\n"
+            b"property uchar blue\nend_header\n")
+    assert raw.startswith(head) and len(raw) == len(head) + 15 * len(P)
+    rec = np.frombuffer(raw[len(head):], dtype=[("x", "<f4"), ("y", "<f4"), ("z", "<f4"),
+                                                ("r", "u1"), ("g", "u1"), ("b", "u1")])
+    np.testing.assert_array_equal(np.stack([rec["x"], rec["y"], rec["z"]], 1), P.astype(np.float32))
+    np.testing.assert_array_equal(np.stack([rec["b"], rec["g"], rec["r"]], 1), C)
+    P2, C2 = ply.read_ply(str(f))
+    np.testing.assert_array_equal(P2, P.astype(np.float32).astype(np.float64))
+    np.testing.assert_array_equal(C2, C)
+    ply.save_ply(P[:0], C[:0], str(f), binary=True)
+    assert ply.read_ply(str(f))[0].shape == (0, 3)
+
+
+@pytest.mark.parametrize("name", ["sl_generate_cloud_e2e", "mp_fixed_mask"])
+def test_read_ply_ascii_reference_file(name, tmp_path):
+    """read_ply on the reference's own ASCII PLY: %.4f values, BGR order back."""
+    d = g.load(name)
+    f = tmp_path / "r.ply"
+    f.write_text(g.ply_text(d["meta"]["ply"]))
+    P, C = ply.read_ply(str(f))
+    expect = np.array([[float(f"{v:.4f}") for v in p] for p in d["P"]]).reshape(-1, 3)
+    np.testing.assert_array_equal(P, expect)
+    np.testing.assert_array_equal(C, d["C"])
