@@ -168,6 +168,36 @@ int sl_write_ply(const char* path, const void* xyz, int xyz_dtype, const uint8_t
 int sl_write_ply_binary(const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n,
                         int threads);
 
+/* ---- merge stage (server/processing.py:116-182) ----
+ * Open3D's PointCloud::VoxelDownSample and RemoveStatisticalOutliers on a
+ * device cloud (xyz f64 [n][3], bgr u8 [n][3] or NULL).  Blocking on `stream`;
+ * counts are returned on the host.  Parity vs Open3D is unpinned (not in this
+ * image): oracle/merge_oracle.py restates the algorithms. */
+
+/* One point per occupied voxel of edge voxel_size, grid origin min - voxel_size/2:
+ * the mean of its points (summed in ascending index, f64) and of its colours
+ * (as c/255, written back as round(clamp(mean)*255)).  Output in ascending
+ * voxel key (ix, iy, iz) (Open3D: hash order); out arrays hold n points.
+ * SL_EINVAL for voxel_size <= 0, "voxel_size is too small." (Open3D's check),
+ * or a grid over 2e6 voxels per axis. */
+int sl_voxel_downsample(sl_ctx* ctx, const double* xyz, const uint8_t* bgr, int64_t n, double voxel_size,
+                        double* out_xyz, uint8_t* out_bgr, int64_t* out_n, void* stream);
+
+/* Mean distance to the nb_neighbors (<= 32) nearest points, the point itself
+ * included (exact kNN, f64) -> avg_dist[n] (device); keeps
+ * 0 < avg < mean + std_ratio * std (Bessel): their indices, ascending, ->
+ * out_index (device, capacity n), the count -> *out_n. */
+int sl_statistical_outliers(sl_ctx* ctx, const double* xyz, int64_t n, int nb_neighbors, double std_ratio,
+                            double* avg_dist, int64_t* out_index, int64_t* out_n, void* stream);
+
+/* select_by_index: out[j] = in[index[j]] (device; bgr optional).  Asynchronous. */
+int sl_select_by_index(sl_ctx* ctx, const double* xyz, const uint8_t* bgr, const int64_t* index, int64_t m,
+                       double* out_xyz, uint8_t* out_bgr, void* stream);
+
+/* In place p' = M p for a row-major 4x4 pose (device), rows in the order
+ * ((m0 x + m1 y) + m2 z) + m3 -- PointCloud::Transform.  Asynchronous. */
+int sl_transform_points(sl_ctx* ctx, double* xyz, int64_t n, const double* pose, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,7 +33,8 @@ SL_XYZ_F32_FAST = 2
 EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_error", "sl_ctx_reserve",
            "sl_set_calib", "sl_decode_triangulate", "sl_triangulate_maps", "sl_sync",
            "sl_last_thresholds", "sl_profile_enable", "sl_profile_read", "sl_format_ply", "sl_write_ply",
-           "sl_write_ply_binary")
+           "sl_write_ply_binary", "sl_voxel_downsample", "sl_statistical_outliers", "sl_select_by_index",
+           "sl_transform_points")
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -58,6 +59,10 @@ _SIGS = {
     "sl_format_ply": (_i32, [_vp, _i32, _vp, _i64, _i32, _vp, _i64, ctypes.POINTER(_i64)]),
     "sl_write_ply": (_i32, [ctypes.c_char_p, _vp, _i32, _vp, _i64, _i32]),
     "sl_write_ply_binary": (_i32, [ctypes.c_char_p, _vp, _i32, _vp, _i64, _i32]),
+    "sl_voxel_downsample": (_i32, [_vp, _vp, _vp, _i64, ctypes.c_double, _vp, _vp, ctypes.POINTER(_i64), _vp]),
+    "sl_statistical_outliers": (_i32, [_vp, _vp, _i64, _i32, ctypes.c_double, _vp, _vp, ctypes.POINTER(_i64), _vp]),
+    "sl_select_by_index": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "sl_transform_points": (_i32, [_vp, _vp, _i64, _vp, _vp]),
 }
 
 _lock = threading.Lock()

@@ -1403,6 +1403,10 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
 
 }  // namespace
 
+// helpers for slmerge.hip (same library)
+int slgpu_fail(sl_ctx* c, int code, const char* msg) { return fail(c, code, msg); }
+int slgpu_device(const sl_ctx* c) { return c->device; }
+
 // ------------------------------------------------------------- PLY writer ----
 // The ASCII PLY of sl_system.py:665-691 (== multi_point_cloud_process.py:
 // 121-131): header, then per point f"{x:.4f} {y:.4f} {z:.4f} {r} {g} {b}\n"

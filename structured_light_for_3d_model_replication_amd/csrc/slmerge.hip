@@ -1,0 +1,715 @@
+// libslgpu.so, part 2 -- the merge stage after the per-view clouds (SURVEY.md
+// §8(f)-3, server/processing.py:116-182): voxel downsample and statistical
+// outlier removal of the merged cloud, as Open3D's PointCloud::VoxelDownSample
+// and PointCloud::RemoveStatisticalOutliers compute them (Open3D is not in
+// this image: the algorithms are restated from its published source, and
+// parity is unpinned -- oracle/merge_oracle.py is the CPU restatement the
+// tests check against).
+//
+//   voxel downsample: min bound (exact reduction) -> linear voxel key of every
+//     point, (p - (min - vs/2)) / vs floored per axis -> stable LSD radix sort
+//     of (key, index) -> per voxel, the sums of its points and colours in
+//     ascending point index (Open3D's AddPoint order, so the f64 sums are
+//     bit-identical) / count.  Output in ascending voxel key (Open3D: hash
+//     order).
+//   statistical outliers: exact k nearest neighbours (the point itself
+//     included, nanoflann's ((dx^2 + dy^2) + dz^2) in f64) on a uniform grid of
+//     sorted cells, searched ring by ring until the k-th distance is inside the
+//     searched cube; mean of the k square roots in ascending order; the cloud
+//     mean / std (Bessel) of those means are sequential sums on the host, as
+//     std::accumulate / std::inner_product do them; keep 0 < mean < cloud_mean
+//     + std_ratio * std.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <limits>
+#include <vector>
+
+#include "slgpu.h"
+
+#pragma clang fp contract(off)
+
+// from slgpu.hip
+int slgpu_fail(sl_ctx* c, int code, const char* msg);
+int slgpu_device(const sl_ctx* c);
+
+namespace {
+
+constexpr int kT = 256;
+constexpr int kRsItems = 16;                // keys per thread in a radix-sort tile
+constexpr int kRsTile = kT * kRsItems;      // 4096
+constexpr int kRsBits = 4;                  // digit width
+constexpr int kRsBins = 1 << kRsBits;
+constexpr int kMaxK = 32;                   // largest nb_neighbors
+
+#define MTRY(ctx, expr)                                                  \
+  do {                                                                   \
+    hipError_t e_ = (expr);                                              \
+    if (e_ != hipSuccess) return slgpu_fail((ctx), SL_EHIP, hipGetErrorString(e_)); \
+  } while (0)
+
+// ------------------------------------------------------------------ bounds ----
+__global__ __launch_bounds__(kT) void k_bounds(const double* xyz, int64_t n, double* part) {
+  __shared__ double s[6][kT];
+  double v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * kT) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double x = xyz[3 * i + k];
+      v[k] = fmin(v[k], x);
+      v[3 + k] = fmax(v[3 + k], x);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) s[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int w = kT / 2; w > 0; w >>= 1) {
+    if (static_cast<int>(threadIdx.x) < w) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        s[k][threadIdx.x] = fmin(s[k][threadIdx.x], s[k][threadIdx.x + w]);
+        s[3 + k][threadIdx.x] = fmax(s[3 + k][threadIdx.x], s[3 + k][threadIdx.x + w]);
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) part[6 * blockIdx.x + threadIdx.x] = s[threadIdx.x][0];
+}
+
+// ------------------------------------------------------- grid cell keys ----
+// key = (ix * ny + iy) * nz + iz with i_a = floor((p_a - lo_a) / h); index = i.
+__global__ __launch_bounds__(kT) void k_cell_keys(const double* xyz, int64_t n, double lo0, double lo1, double lo2,
+                                                  double h, int64_t ny, int64_t nz, uint64_t* keys, uint32_t* vals) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i >= n) return;
+  const int64_t ix = static_cast<int64_t>(floor((xyz[3 * i] - lo0) / h));
+  const int64_t iy = static_cast<int64_t>(floor((xyz[3 * i + 1] - lo1) / h));
+  const int64_t iz = static_cast<int64_t>(floor((xyz[3 * i + 2] - lo2) / h));
+  keys[i] = static_cast<uint64_t>((ix * ny + iy) * nz + iz);
+  vals[i] = static_cast<uint32_t>(i);
+}
+
+// ---------------------------------------------------------- radix sort ----
+// Stable LSD sort of (uint64 key, uint32 value), kRsBits per pass.  A pass:
+// per-tile digit counts (digit-major), one exclusive scan over them, and a
+// scatter in which every key's rank inside its tile is the count of equal
+// digits before it (thread-contiguous items, so the order is stable).
+__device__ __forceinline__ unsigned digit_of(uint64_t k, int shift) {
+  return static_cast<unsigned>(k >> shift) & (kRsBins - 1);
+}
+
+__global__ __launch_bounds__(kT) void k_rs_count(const uint64_t* keys, int64_t n, int shift, uint32_t* counts,
+                                                 int tiles) {
+  __shared__ uint32_t s_c[kRsBins];
+  if (threadIdx.x < kRsBins) s_c[threadIdx.x] = 0u;
+  __syncthreads();
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile + static_cast<int64_t>(threadIdx.x) * kRsItems;
+  uint32_t c[kRsBins];
+#pragma unroll
+  for (int d = 0; d < kRsBins; ++d) c[d] = 0u;
+#pragma unroll
+  for (int j = 0; j < kRsItems; ++j) {
+    if (base + j < n) {
+      const unsigned d = digit_of(keys[base + j], shift);
+#pragma unroll
+      for (int e = 0; e < kRsBins; ++e) c[e] += (d == static_cast<unsigned>(e)) ? 1u : 0u;
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < kRsBins; ++d)
+    if (c[d]) atomicAdd(&s_c[d], c[d]);
+  __syncthreads();
+  if (threadIdx.x < kRsBins) counts[static_cast<int64_t>(threadIdx.x) * tiles + blockIdx.x] = s_c[threadIdx.x];
+}
+
+// Exclusive scan of a uint32 array by one workgroup (thread t owns a
+// contiguous stretch); the total goes to *total when non-null.
+__global__ __launch_bounds__(kT) void k_scan1(uint32_t* a, int64_t n, uint32_t* total) {
+  __shared__ uint32_t s[kT];
+  const int64_t per = (n + kT - 1) / kT;
+  const int64_t lo = min<int64_t>(n, threadIdx.x * per), hi = min<int64_t>(n, lo + per);
+  uint32_t sum = 0u;
+  for (int64_t i = lo; i < hi; ++i) sum += a[i];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0u;
+    for (int t = 0; t < kT; ++t) {
+      const uint32_t v = s[t];
+      s[t] = run;
+      run += v;
+    }
+    if (total) *total = run;
+  }
+  __syncthreads();
+  uint32_t run = s[threadIdx.x];
+  for (int64_t i = lo; i < hi; ++i) {
+    const uint32_t v = a[i];
+    a[i] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(kT) void k_rs_scatter(const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
+                                                   uint32_t* vout, int64_t n, int shift, const uint32_t* offs,
+                                                   int tiles) {
+  __shared__ uint32_t s[kRsBins * kT];  // [digit][thread] counts, then their exclusive scan
+  __shared__ uint32_t s_part[kT];
+  const int t = threadIdx.x;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile + static_cast<int64_t>(t) * kRsItems;
+  uint64_t k[kRsItems];
+  uint32_t v[kRsItems];
+  unsigned dg[kRsItems];
+  uint32_t c[kRsBins];
+#pragma unroll
+  for (int d = 0; d < kRsBins; ++d) c[d] = 0u;
+#pragma unroll
+  for (int j = 0; j < kRsItems; ++j) {
+    const bool ok = base + j < n;
+    k[j] = ok ? kin[base + j] : 0ull;
+    v[j] = ok ? vin[base + j] : 0u;
+    dg[j] = ok ? digit_of(k[j], shift) : kRsBins;  // kRsBins: no item
+#pragma unroll
+    for (int e = 0; e < kRsBins; ++e) c[e] += (dg[j] == static_cast<unsigned>(e)) ? 1u : 0u;
+  }
+#pragma unroll
+  for (int d = 0; d < kRsBins; ++d) s[d * kT + t] = c[d];
+  __syncthreads();
+  // exclusive scan of s[] (digit-major): thread t owns entries [16 t, 16 t + 16)
+  uint32_t loc[kRsBins];
+  uint32_t sum = 0u;
+#pragma unroll
+  for (int j = 0; j < kRsBins; ++j) {
+    loc[j] = sum;
+    sum += s[kRsBins * t + j];
+  }
+  s_part[t] = sum;
+  __syncthreads();
+  if (t < 64) {  // scan of the 256 partial sums by one wave (4 per lane)
+    uint32_t a0 = s_part[4 * t], a1 = s_part[4 * t + 1], a2 = s_part[4 * t + 2], a3 = s_part[4 * t + 3];
+    const uint32_t tot = a0 + a1 + a2 + a3;
+    uint32_t inc = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (t >= d) inc += y;
+    }
+    uint32_t ex = inc - tot;
+    s_part[4 * t] = ex;
+    ex += a0;
+    s_part[4 * t + 1] = ex;
+    ex += a1;
+    s_part[4 * t + 2] = ex;
+    ex += a2;
+    s_part[4 * t + 3] = ex;
+  }
+  __syncthreads();
+  const uint32_t pre = s_part[t];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRsBins; ++j) s[kRsBins * t + j] = pre + loc[j];
+  __syncthreads();
+  // item j of thread t with digit d: global offset of (d, tile) + (d's items in
+  // earlier threads of the tile) + (d's items earlier in this thread)
+  uint32_t run[kRsBins];
+#pragma unroll
+  for (int d = 0; d < kRsBins; ++d) run[d] = 0u;
+#pragma unroll
+  for (int j = 0; j < kRsItems; ++j) {
+    if (dg[j] < static_cast<unsigned>(kRsBins)) {
+      const unsigned d = dg[j];
+      uint32_t r = 0u;
+#pragma unroll
+      for (int e = 0; e < kRsBins; ++e)
+        if (d == static_cast<unsigned>(e)) {
+          r = run[e];
+          ++run[e];
+        }
+      const uint32_t pos =
+          offs[static_cast<int64_t>(d) * tiles + blockIdx.x] + (s[d * kT + t] - s[d * kT]) + r;
+      kout[pos] = k[j];
+      vout[pos] = v[j];
+    }
+  }
+}
+
+// ------------------------------------------------------------- segments ----
+__global__ __launch_bounds__(kT) void k_heads(const uint64_t* keys, int64_t n, uint32_t* flag) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i < n) flag[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1u : 0u;
+}
+
+// Exclusive scan of flag[] (multi-workgroup: per-workgroup sums, one
+// workgroup scanning them, then the local scans); total -> *total.
+__global__ __launch_bounds__(kT) void k_tile_sums(const uint32_t* a, int64_t n, uint32_t* sums) {
+  __shared__ uint32_t s[kT];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile + static_cast<int64_t>(threadIdx.x) * kRsItems;
+  uint32_t sum = 0u;
+#pragma unroll
+  for (int j = 0; j < kRsItems; ++j)
+    if (base + j < n) sum += a[base + j];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (int w = kT / 2; w > 0; w >>= 1) {
+    if (static_cast<int>(threadIdx.x) < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sums[blockIdx.x] = s[0];
+}
+
+__global__ __launch_bounds__(kT) void k_tile_scan(const uint32_t* a, int64_t n, const uint32_t* sums, uint32_t* out) {
+  __shared__ uint32_t s[kT];
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile + static_cast<int64_t>(threadIdx.x) * kRsItems;
+  uint32_t v[kRsItems];
+  uint32_t sum = 0u;
+#pragma unroll
+  for (int j = 0; j < kRsItems; ++j) {
+    v[j] = base + j < n ? a[base + j] : 0u;
+    sum += v[j];
+  }
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = sums[blockIdx.x];
+    for (int t = 0; t < kT; ++t) {
+      const uint32_t x = s[t];
+      s[t] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+  uint32_t run = s[threadIdx.x];
+#pragma unroll
+  for (int j = 0; j < kRsItems; ++j) {
+    if (base + j < n) out[base + j] = run;
+    run += v[j];
+  }
+}
+
+__global__ __launch_bounds__(kT) void k_seg_starts(const uint32_t* flag, const uint32_t* seg, const uint64_t* keys,
+                                                   int64_t n, uint32_t* starts, uint64_t* ukeys) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i < n && flag[i]) {
+    starts[seg[i]] = static_cast<uint32_t>(i);
+    ukeys[seg[i]] = keys[i];
+  }
+}
+
+// One voxel per thread: its points in ascending index, summed in that order
+// (AccumulatedPoint::AddPoint), averaged (GetAveragePoint / GetAverageColor);
+// colours as Open3D holds them (c / 255.0) and writes them (round(clamp * 255)).
+__global__ __launch_bounds__(kT) void k_voxel_avg(const uint32_t* starts, int64_t n_vox, int64_t n,
+                                                  const uint32_t* idx, const double* xyz, const uint8_t* bgr,
+                                                  double* oxyz, uint8_t* obgr) {
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (s >= n_vox) return;
+  const int64_t a = starts[s], b = s + 1 < n_vox ? static_cast<int64_t>(starts[s + 1]) : n;
+  double p0 = 0.0, p1 = 0.0, p2 = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
+  for (int64_t j = a; j < b; ++j) {
+    const int64_t i = idx[j];
+    p0 += xyz[3 * i];
+    p1 += xyz[3 * i + 1];
+    p2 += xyz[3 * i + 2];
+    if (bgr) {
+      c0 += static_cast<double>(bgr[3 * i]) / 255.0;
+      c1 += static_cast<double>(bgr[3 * i + 1]) / 255.0;
+      c2 += static_cast<double>(bgr[3 * i + 2]) / 255.0;
+    }
+  }
+  const double m = static_cast<double>(b - a);
+  oxyz[3 * s] = p0 / m;
+  oxyz[3 * s + 1] = p1 / m;
+  oxyz[3 * s + 2] = p2 / m;
+  if (bgr && obgr) {
+    const double cc[3] = {c0 / m, c1 / m, c2 / m};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) obgr[3 * s + k] = static_cast<uint8_t>(round(fmin(1.0, fmax(0.0, cc[k])) * 255.0));
+  }
+}
+
+// ------------------------------------------------------------------ kNN ----
+struct Grid {
+  double lo0, lo1, lo2, h;
+  int64_t nx, ny, nz;
+};
+
+__device__ __forceinline__ int64_t find_cell(const uint64_t* ukeys, int64_t m, uint64_t key) {
+  int64_t a = 0, b = m;  // first >= key
+  while (a < b) {
+    const int64_t c = (a + b) >> 1;
+    if (ukeys[c] < key) a = c + 1;
+    else b = c;
+  }
+  return (a < m && ukeys[a] == key) ? a : -1;
+}
+
+// Mean distance to the k nearest points (the point itself included) of every
+// point, in the order of the cell-sorted points (one query per thread).
+__global__ __launch_bounds__(kT) void k_knn_mean(const double* xyz, int64_t n, const uint32_t* sidx,
+                                                 const uint64_t* ukeys, const uint32_t* ustart, int64_t m, Grid g,
+                                                 int k, double* avg) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (j >= n) return;
+  const int64_t qi = sidx[j];
+  const double q0 = xyz[3 * qi], q1 = xyz[3 * qi + 1], q2 = xyz[3 * qi + 2];
+  const int64_t cx = static_cast<int64_t>(floor((q0 - g.lo0) / g.h));
+  const int64_t cy = static_cast<int64_t>(floor((q1 - g.lo1) / g.h));
+  const int64_t cz = static_cast<int64_t>(floor((q2 - g.lo2) / g.h));
+  double bd[kMaxK];
+#pragma unroll
+  for (int e = 0; e < kMaxK; ++e) bd[e] = INFINITY;
+  double kth = INFINITY;  // bd[k - 1]
+  int64_t found = 0;
+  const int64_t kk = min<int64_t>(k, n);
+  for (int64_t r = 0;; ++r) {
+    for (int64_t dx = -r; dx <= r; ++dx) {
+      const int64_t x = cx + dx;
+      if (x < 0 || x >= g.nx) continue;
+      for (int64_t dy = -r; dy <= r; ++dy) {
+        const int64_t y = cy + dy;
+        if (y < 0 || y >= g.ny) continue;
+        const bool edge = (dx == -r || dx == r || dy == -r || dy == r);
+        for (int64_t dz = -r; dz <= r; dz += (edge ? 1 : 2 * r > 0 ? 2 * r : 1)) {
+          const int64_t z = cz + dz;
+          if (z < 0 || z >= g.nz) continue;
+          const int64_t c = find_cell(ukeys, m, static_cast<uint64_t>((x * g.ny + y) * g.nz + z));
+          if (c < 0) continue;
+          const int64_t a = ustart[c], b = c + 1 < m ? static_cast<int64_t>(ustart[c + 1]) : n;
+          for (int64_t t = a; t < b; ++t) {
+            const int64_t pi = sidx[t];
+            const double d0 = q0 - xyz[3 * pi], d1 = q1 - xyz[3 * pi + 1], d2 = q2 - xyz[3 * pi + 2];
+            const double dd = ((d0 * d0) + d1 * d1) + d2 * d2;  // nanoflann L2_Adaptor order for 3 dims
+            ++found;
+            if (dd < kth || found <= kk) {
+              double v = dd;
+#pragma unroll
+              for (int e = 0; e < kMaxK; ++e) {
+                const double lo = fmin(bd[e], v), hi = fmax(bd[e], v);
+                bd[e] = lo;
+                v = hi;
+              }
+              double t2 = bd[0];
+#pragma unroll
+              for (int e = 1; e < kMaxK; ++e)
+                if (e == kk - 1) t2 = bd[e];
+              kth = t2;
+            }
+          }
+        }
+      }
+    }
+    // every point outside the searched cube is at least `bound` away
+    const double lo0 = g.lo0 + static_cast<double>(cx - r) * g.h, hi0 = g.lo0 + static_cast<double>(cx + r + 1) * g.h;
+    const double lo1 = g.lo1 + static_cast<double>(cy - r) * g.h, hi1 = g.lo1 + static_cast<double>(cy + r + 1) * g.h;
+    const double lo2 = g.lo2 + static_cast<double>(cz - r) * g.h, hi2 = g.lo2 + static_cast<double>(cz + r + 1) * g.h;
+    double bound = fmin(fmin(q0 - lo0, hi0 - q0), fmin(fmin(q1 - lo1, hi1 - q1), fmin(q2 - lo2, hi2 - q2)));
+    // margin for points filed into a neighbouring cell by the rounding of (p - lo) / h
+    bound -= 1e-12 * (fabs(q0) + fabs(q1) + fabs(q2) + fabs(g.lo0) + fabs(g.lo1) + fabs(g.lo2) + g.h);
+    bound = fmax(bound, 0.0);
+    const bool all = cx - r <= 0 && cy - r <= 0 && cz - r <= 0 && cx + r >= g.nx - 1 && cy + r >= g.ny - 1 &&
+                     cz + r >= g.nz - 1;
+    if (all || (found >= kk && kth < bound * bound)) break;
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int e = 0; e < kMaxK; ++e)
+    if (e < kk) s += sqrt(bd[e]);
+  avg[qi] = kk > 0 ? s / static_cast<double>(kk) : -1.0;
+}
+
+__global__ __launch_bounds__(kT) void k_keep_flags(const double* avg, int64_t n, double thr, uint32_t* flag) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i < n) flag[i] = (avg[i] > 0.0 && avg[i] < thr) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kT) void k_compact_index(const uint32_t* flag, const uint32_t* pos, int64_t n,
+                                                      int64_t* out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i < n && flag[i]) out[pos[i]] = i;
+}
+
+__global__ __launch_bounds__(kT) void k_gather(const double* xyz, const uint8_t* bgr, const int64_t* idx, int64_t m,
+                                               double* oxyz, uint8_t* obgr) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (j >= m) return;
+  const int64_t i = idx[j];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) oxyz[3 * j + k] = xyz[3 * i + k];
+  if (bgr && obgr)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) obgr[3 * j + k] = bgr[3 * i + k];
+}
+
+// p' = M p for a 4x4 row-major pose: row r = ((m_r0 x + m_r1 y) + m_r2 z) + m_r3
+// (Eigen's (M * (x, y, z, 1)).head<3>() in PointCloud::Transform), in place.
+__global__ __launch_bounds__(kT) void k_transform(double* xyz, int64_t n, const double* m) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i >= n) return;
+  const double x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) xyz[3 * i + r] = ((m[4 * r] * x + m[4 * r + 1] * y) + m[4 * r + 2] * z) + m[4 * r + 3];
+}
+
+// ------------------------------------------------------------------ host ----
+unsigned blocks(int64_t n) { return static_cast<unsigned>((n + kT - 1) / kT); }
+
+template <typename T>
+struct DBuf {
+  T* p = nullptr;
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t alloc(int64_t n) { return hipMalloc(reinterpret_cast<void**>(&p), sizeof(T) * std::max<int64_t>(n, 1)); }
+};
+
+// min / max bound of n points (device) -> host b[6]
+int bounds(sl_ctx* c, const double* xyz, int64_t n, double* b, hipStream_t s) {
+  const int nb = static_cast<int>(std::min<int64_t>(1024, (n + kT - 1) / kT));
+  DBuf<double> part;
+  MTRY(c, part.alloc(6 * nb));
+  hipLaunchKernelGGL(k_bounds, dim3(nb), dim3(kT), 0, s, xyz, n, part.p);
+  MTRY(c, hipGetLastError());
+  std::vector<double> h(6 * static_cast<size_t>(nb));
+  MTRY(c, hipMemcpyAsync(h.data(), part.p, sizeof(double) * h.size(), hipMemcpyDeviceToHost, s));
+  MTRY(c, hipStreamSynchronize(s));
+  for (int k = 0; k < 3; ++k) {
+    b[k] = INFINITY;
+    b[3 + k] = -INFINITY;
+  }
+  for (int i = 0; i < nb; ++i)
+    for (int k = 0; k < 3; ++k) {
+      b[k] = std::min(b[k], h[6 * i + k]);
+      b[3 + k] = std::max(b[3 + k], h[6 * i + 3 + k]);
+    }
+  return SL_OK;
+}
+
+// Stable sort of (keys, vals) in place (device), over the low `bits` bits.
+int radix_sort(sl_ctx* c, uint64_t* keys, uint32_t* vals, int64_t n, int bits, hipStream_t s) {
+  const int tiles = static_cast<int>((n + kRsTile - 1) / kRsTile);
+  DBuf<uint64_t> k2;
+  DBuf<uint32_t> v2, cnt;
+  MTRY(c, k2.alloc(n));
+  MTRY(c, v2.alloc(n));
+  MTRY(c, cnt.alloc(static_cast<int64_t>(kRsBins) * tiles));
+  uint64_t *ka = keys, *kb = k2.p;
+  uint32_t *va = vals, *vb = v2.p;
+  int passes = 0;
+  for (int shift = 0; shift < bits; shift += kRsBits, ++passes) {
+    hipLaunchKernelGGL(k_rs_count, dim3(tiles), dim3(kT), 0, s, ka, n, shift, cnt.p, tiles);
+    hipLaunchKernelGGL(k_scan1, dim3(1), dim3(kT), 0, s, cnt.p, static_cast<int64_t>(kRsBins) * tiles,
+                       static_cast<uint32_t*>(nullptr));
+    hipLaunchKernelGGL(k_rs_scatter, dim3(tiles), dim3(kT), 0, s, ka, va, kb, vb, n, shift, cnt.p, tiles);
+    MTRY(c, hipGetLastError());
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  if (passes & 1) {  // result is in the scratch pair
+    MTRY(c, hipMemcpyAsync(keys, ka, sizeof(uint64_t) * n, hipMemcpyDeviceToDevice, s));
+    MTRY(c, hipMemcpyAsync(vals, va, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, s));
+  }
+  MTRY(c, hipStreamSynchronize(s));  // scratch is freed on return
+  return SL_OK;
+}
+
+// Exclusive scan of flag[0..n) -> pos; returns the total on the host.
+int scan_flags(sl_ctx* c, const uint32_t* flag, int64_t n, uint32_t* pos, int64_t* total, hipStream_t s) {
+  const int tiles = static_cast<int>((n + kRsTile - 1) / kRsTile);
+  DBuf<uint32_t> sums, tot;
+  MTRY(c, sums.alloc(tiles));
+  MTRY(c, tot.alloc(1));
+  hipLaunchKernelGGL(k_tile_sums, dim3(tiles), dim3(kT), 0, s, flag, n, sums.p);
+  hipLaunchKernelGGL(k_scan1, dim3(1), dim3(kT), 0, s, sums.p, static_cast<int64_t>(tiles), tot.p);
+  hipLaunchKernelGGL(k_tile_scan, dim3(tiles), dim3(kT), 0, s, flag, n, sums.p, pos);
+  MTRY(c, hipGetLastError());
+  uint32_t t = 0;
+  MTRY(c, hipMemcpyAsync(&t, tot.p, sizeof(t), hipMemcpyDeviceToHost, s));
+  MTRY(c, hipStreamSynchronize(s));
+  *total = t;
+  return SL_OK;
+}
+
+int key_bits(uint64_t max_key) {
+  int b = 0;
+  while (b < 64 && (max_key >> b) != 0) ++b;
+  return std::max(b, 1);
+}
+
+// Grid over [lo, hi] with cell h: dims, checked so that linear keys fit 63 bits.
+bool make_grid(const double* lo, const double* hi, double h, Grid* g) {
+  int64_t d[3];
+  for (int k = 0; k < 3; ++k) {
+    const double e = floor((hi[k] - lo[k]) / h);
+    if (!(e >= 0.0) || e > 2.0e6) return false;
+    d[k] = static_cast<int64_t>(e) + 1;
+  }
+  if (static_cast<double>(d[0]) * static_cast<double>(d[1]) * static_cast<double>(d[2]) > 9.0e18) return false;
+  g->lo0 = lo[0];
+  g->lo1 = lo[1];
+  g->lo2 = lo[2];
+  g->h = h;
+  g->nx = d[0];
+  g->ny = d[1];
+  g->nz = d[2];
+  return true;
+}
+
+// Sort the points into grid cells: sorted keys + point indices, and the
+// unique cells with their first position.  Returns the cell count in *m.
+int cells(sl_ctx* c, const double* xyz, int64_t n, const Grid& g, DBuf<uint64_t>& keys, DBuf<uint32_t>& idx,
+          DBuf<uint64_t>& ukeys, DBuf<uint32_t>& ustart, int64_t* m, hipStream_t s) {
+  MTRY(c, keys.alloc(n));
+  MTRY(c, idx.alloc(n));
+  hipLaunchKernelGGL(k_cell_keys, dim3(blocks(n)), dim3(kT), 0, s, xyz, n, g.lo0, g.lo1, g.lo2, g.h, g.ny, g.nz,
+                     keys.p, idx.p);
+  MTRY(c, hipGetLastError());
+  const uint64_t max_key = static_cast<uint64_t>((g.nx * g.ny) * g.nz - 1);
+  int r = radix_sort(c, keys.p, idx.p, n, key_bits(max_key), s);
+  if (r) return r;
+  DBuf<uint32_t> flag, seg;
+  MTRY(c, flag.alloc(n));
+  MTRY(c, seg.alloc(n));
+  hipLaunchKernelGGL(k_heads, dim3(blocks(n)), dim3(kT), 0, s, keys.p, n, flag.p);
+  r = scan_flags(c, flag.p, n, seg.p, m, s);
+  if (r) return r;
+  MTRY(c, ustart.alloc(*m));
+  MTRY(c, ukeys.alloc(*m));
+  hipLaunchKernelGGL(k_seg_starts, dim3(blocks(n)), dim3(kT), 0, s, flag.p, seg.p, keys.p, n, ustart.p, ukeys.p);
+  MTRY(c, hipGetLastError());
+  MTRY(c, hipStreamSynchronize(s));
+  return SL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sl_voxel_downsample(sl_ctx* c, const double* xyz, const uint8_t* bgr, int64_t n, double voxel_size,
+                        double* out_xyz, uint8_t* out_bgr, int64_t* out_n, void* stream) {
+  if (!c || !out_n || n < 0 || (n && (!xyz || !out_xyz))) return SL_EINVAL;
+  if (!(voxel_size > 0.0)) return slgpu_fail(c, SL_EINVAL, "voxel_size <= 0.");
+  if (n >= (1ll << 31)) return slgpu_fail(c, SL_EINVAL, "at most 2^31 - 1 points");
+  *out_n = 0;
+  if (n == 0) return SL_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  MTRY(c, hipSetDevice(slgpu_device(c)));
+  double b[6];
+  int r = bounds(c, xyz, n, b, s);
+  if (r) return r;
+  // voxel_min_bound = min - vs/2, voxel_max_bound = max + vs/2 (VoxelDownSample)
+  double lo[3], hi[3];
+  for (int k = 0; k < 3; ++k) {
+    lo[k] = b[k] - voxel_size * 0.5;
+    hi[k] = b[3 + k] + voxel_size * 0.5;
+  }
+  double ext = 0.0;
+  for (int k = 0; k < 3; ++k) ext = std::max(ext, hi[k] - lo[k]);
+  if (voxel_size * std::numeric_limits<int>::max() < ext) return slgpu_fail(c, SL_EINVAL, "voxel_size is too small.");
+  Grid g;
+  if (!make_grid(lo, b + 3, voxel_size, &g))
+    return slgpu_fail(c, SL_EINVAL, "voxel grid exceeds 2e6 voxels per axis / 2^63 voxels");
+  DBuf<uint64_t> keys, ukeys;
+  DBuf<uint32_t> idx, ustart;
+  int64_t m = 0;
+  r = cells(c, xyz, n, g, keys, idx, ukeys, ustart, &m, s);
+  if (r) return r;
+  hipLaunchKernelGGL(k_voxel_avg, dim3(blocks(m)), dim3(kT), 0, s, ustart.p, m, n, idx.p, xyz, bgr, out_xyz,
+                     out_bgr);
+  MTRY(c, hipGetLastError());
+  MTRY(c, hipStreamSynchronize(s));
+  *out_n = m;
+  return SL_OK;
+}
+
+int sl_statistical_outliers(sl_ctx* c, const double* xyz, int64_t n, int nb_neighbors, double std_ratio,
+                            double* avg_dist, int64_t* out_index, int64_t* out_n, void* stream) {
+  if (!c || !out_n || n < 0 || (n && (!xyz || !avg_dist || !out_index))) return SL_EINVAL;
+  if (nb_neighbors < 1 || !(std_ratio > 0.0))
+    return slgpu_fail(c, SL_EINVAL, "Illegal input parameters, number of neighbors and standard deviation ratio "
+                                    "must be positive");
+  if (nb_neighbors > kMaxK) return slgpu_fail(c, SL_EINVAL, "nb_neighbors > 32 is not supported");
+  if (n >= (1ll << 31)) return slgpu_fail(c, SL_EINVAL, "at most 2^31 - 1 points");
+  *out_n = 0;
+  if (n == 0) return SL_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  MTRY(c, hipSetDevice(slgpu_device(c)));
+  double b[6];
+  int r = bounds(c, xyz, n, b, s);
+  if (r) return r;
+  // cell size: about k points per cell for a volume-filling cloud (surfaces
+  // put more per occupied cell); exactness does not depend on it
+  double ext[3], vol = 1.0, emax = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    ext[k] = b[3 + k] - b[k];
+    emax = std::max(emax, ext[k]);
+  }
+  for (int k = 0; k < 3; ++k) vol *= std::max(ext[k], emax * 1e-3);
+  double h = cbrt(vol * nb_neighbors / static_cast<double>(n));
+  h = std::max(h, emax / 1.0e6);
+  if (!(h > 0.0) || !std::isfinite(h)) h = 1.0;  // all points coincide (or non-finite input)
+  Grid g;
+  while (!make_grid(b, b + 3, h, &g)) h *= 2.0;
+  DBuf<uint64_t> keys, ukeys;
+  DBuf<uint32_t> idx, ustart;
+  int64_t m = 0;
+  r = cells(c, xyz, n, g, keys, idx, ukeys, ustart, &m, s);
+  if (r) return r;
+  hipLaunchKernelGGL(k_knn_mean, dim3(blocks(n)), dim3(kT), 0, s, xyz, n, idx.p, ukeys.p, ustart.p, m, g,
+                     nb_neighbors, avg_dist);
+  MTRY(c, hipGetLastError());
+  // cloud mean / std of the positive means: sequential, as std::accumulate /
+  // std::inner_product in RemoveStatisticalOutliers
+  std::vector<double> a(static_cast<size_t>(n));
+  MTRY(c, hipMemcpyAsync(a.data(), avg_dist, sizeof(double) * a.size(), hipMemcpyDeviceToHost, s));
+  MTRY(c, hipStreamSynchronize(s));
+  int64_t valid = 0;
+  double mean = 0.0;
+  for (double v : a) {
+    if (v > 0) mean = mean + v;
+  }
+  for (double v : a) valid += (v >= 0.0) ? 1 : 0;  // every point has >= 1 neighbour (itself)
+  if (valid == 0) return SL_OK;
+  mean /= static_cast<double>(valid);
+  double sq = 0.0;
+  for (double v : a) sq = sq + (v > 0 ? (v - mean) * (v - mean) : 0);
+  const double sd = sqrt(sq / static_cast<double>(valid - 1));
+  const double thr = mean + std_ratio * sd;
+  DBuf<uint32_t> flag, pos;
+  MTRY(c, flag.alloc(n));
+  MTRY(c, pos.alloc(n));
+  hipLaunchKernelGGL(k_keep_flags, dim3(blocks(n)), dim3(kT), 0, s, avg_dist, n, thr, flag.p);
+  int64_t kept = 0;
+  r = scan_flags(c, flag.p, n, pos.p, &kept, s);
+  if (r) return r;
+  hipLaunchKernelGGL(k_compact_index, dim3(blocks(n)), dim3(kT), 0, s, flag.p, pos.p, n, out_index);
+  MTRY(c, hipGetLastError());
+  MTRY(c, hipStreamSynchronize(s));
+  *out_n = kept;
+  return SL_OK;
+}
+
+int sl_select_by_index(sl_ctx* c, const double* xyz, const uint8_t* bgr, const int64_t* index, int64_t m,
+                       double* out_xyz, uint8_t* out_bgr, void* stream) {
+  if (!c || m < 0 || (m && (!xyz || !index || !out_xyz))) return SL_EINVAL;
+  if (m == 0) return SL_OK;
+  MTRY(c, hipSetDevice(slgpu_device(c)));
+  hipLaunchKernelGGL(k_gather, dim3(blocks(m)), dim3(kT), 0, static_cast<hipStream_t>(stream), xyz, bgr, index, m,
+                     out_xyz, out_bgr);
+  MTRY(c, hipGetLastError());
+  return SL_OK;
+}
+
+int sl_transform_points(sl_ctx* c, double* xyz, int64_t n, const double* pose, void* stream) {
+  if (!c || n < 0 || (n && (!xyz || !pose))) return SL_EINVAL;
+  if (n == 0) return SL_OK;
+  MTRY(c, hipSetDevice(slgpu_device(c)));
+  hipLaunchKernelGGL(k_transform, dim3(blocks(n)), dim3(kT), 0, static_cast<hipStream_t>(stream), xyz, n, pose);
+  MTRY(c, hipGetLastError());
+  return SL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,137 @@
+"""Merge stage on the GPU (csrc/slmerge.hip) vs oracle/merge_oracle.py, bit for
+bit.  Open3D parity is unpinned (not installed); the oracle restates its
+VoxelDownSample / RemoveStatisticalOutliers."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import merge_oracle as mo
+from oracle import sl_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mg():
+    from structured_light_for_3d_model_replication_amd import merge
+    return merge
+
+
+def _cloud(n, seed, scale=300.0):
+    rng = np.random.default_rng(seed)
+    # a bumpy sphere shell + a slab + sparse outliers: surface-like density
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    P = u * (scale * (1 + 0.02 * rng.standard_normal((n, 1))))
+    P[: n // 5, 2] = rng.uniform(-1, 1, n // 5) * 2 - scale * 1.2
+    m = n // 50
+    if m:
+        P[n - m:] = rng.uniform(-2 * scale, 2 * scale, (m, 3))
+    C = rng.integers(0, 256, (n, 3), dtype=np.uint8)
+    return P, C
+
+
+@pytest.mark.parametrize("n,vs", [(50_000, 7.5), (50_000, 30.0), (3_000, 1.0), (1, 0.5)])
+def test_voxel_down_sample_vs_oracle(mg, n, vs):
+    P, C = _cloud(n, seed=n)
+    Q, Cq = mg.voxel_down_sample(P, C, vs)
+    Qe, Ce = mo.voxel_down_sample(P, C, vs)
+    np.testing.assert_array_equal(Q.cpu().numpy(), Qe)
+    np.testing.assert_array_equal(Cq.cpu().numpy(), Ce)
+    Q2, C2 = mg.voxel_down_sample(P, None, vs)
+    assert C2 is None
+    np.testing.assert_array_equal(Q2.cpu().numpy(), Qe)
+
+
+def test_voxel_errors(mg):
+    P, C = _cloud(100, seed=3)
+    with pytest.raises(ValueError):
+        mg.voxel_down_sample(P, C, 0.0)
+    with pytest.raises(ValueError):
+        mg.voxel_down_sample(np.array([[0, 0, 0], [1e9, 0, 0]], float), None, 1e-3)
+    Q, Cq = mg.voxel_down_sample(np.zeros((0, 3)), np.zeros((0, 3), np.uint8), 1.0)
+    assert Q.shape == (0, 3) and Cq.shape == (0, 3)
+
+
+@pytest.mark.parametrize("n,k", [(3_000, 20), (2_500, 1), (2_000, 32), (15, 20)])
+def test_statistical_outliers_vs_oracle(mg, n, k):
+    P, _ = _cloud(n, seed=10 + n)
+    ind, avg = mg.remove_statistical_outlier(P, k, 2.0)
+    ind_e, avg_e = mo.remove_statistical_outlier(P, k, 2.0)
+    np.testing.assert_array_equal(avg.cpu().numpy(), avg_e)
+    np.testing.assert_array_equal(ind.cpu().numpy(), ind_e)
+
+
+def test_statistical_outliers_large_vs_ckdtree(mg):
+    from scipy.spatial import cKDTree
+    P, _ = _cloud(300_000, seed=5)
+    ind, avg = mg.remove_statistical_outlier(P, 20, 2.0)
+    d, _ = cKDTree(P).query(P, k=20)
+    a = avg.cpu().numpy()
+    np.testing.assert_allclose(a, d.mean(1), rtol=1e-14)
+    np.testing.assert_array_equal(ind.cpu().numpy(), mo.statistical_outlier_indices(a, 2.0))
+
+
+def test_statistical_duplicates_and_errors(mg):
+    ind, avg = mg.remove_statistical_outlier(np.ones((40, 3)), 20, 2.0)
+    assert len(ind) == 0 and np.all(avg.cpu().numpy() == 0)
+    P = np.concatenate([np.repeat(np.array([[1.0, 2.0, 3.0]]), 25, 0), _cloud(500, seed=9)[0]])
+    ind, avg = mg.remove_statistical_outlier(P, 20, 2.0)
+    ind_e, avg_e = mo.remove_statistical_outlier(P, 20, 2.0)
+    np.testing.assert_array_equal(avg.cpu().numpy(), avg_e)
+    np.testing.assert_array_equal(ind.cpu().numpy(), ind_e)
+    for bad in [(0, 2.0), (20, 0.0), (33, 2.0)]:
+        with pytest.raises(ValueError):
+            mg.remove_statistical_outlier(P, *bad)
+
+
+def test_transform_and_select(mg):
+    from structured_light_for_3d_model_replication_amd import synth
+    P, C = _cloud(10_000, seed=4)
+    M = synth.turntable_pose(37.0)
+    np.testing.assert_array_equal(mg.transform(P, M).cpu().numpy(), o.apply_pose(P, M))
+    ind = np.array([5, 0, 9999, 17], np.int64)
+    Q, Cq = mg.select_by_index(P, C, ind)
+    np.testing.assert_array_equal(Q.cpu().numpy(), P[ind])
+    np.testing.assert_array_equal(Cq.cpu().numpy(), C[ind])
+    with pytest.raises(IndexError):
+        mg.select_by_index(P, C, np.array([10_000]))
+
+
+def test_merge_posed_views_end_to_end(mg, tmp_path):
+    """Turntable views -> per-view PLYs -> merge_pro_360_posed (poses given)
+    == the oracle pipeline (pose, concat, voxel, SOR, select), then the
+    binary PLY reads back."""
+    from structured_light_for_3d_model_replication_amd import core, ply, synth
+    rig = synth.Rig(H=120, W=160)
+    cal = synth.make_calibration(rig)
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, rig.H, rig.W)
+    degs = [0.0, 30.0, 60.0, 90.0]
+    inv_poses, Ps, Cs = [], [], []
+    for i, deg in enumerate(degs):
+        st, tex = synth.render_stack(rig, seed=70 + i, view_deg=deg)
+        res = eng.decode_triangulate(st.cuda(), texture=tex.cuda(), xyz_dtype=torch.float64)
+        eng.sync()
+        c = res["cloud"]
+        n = c.total()
+        P, C = c.xyz[:n].cpu().numpy(), c.bgr[:n].cpu().numpy()
+        ply.save_ply(P, C, str(tmp_path / f"scan_{i:03d}.ply"))
+        inv_poses.append(synth.turntable_pose(deg))
+        Ps.append(P)
+        Cs.append(C)
+    out = tmp_path / "merged.ply"
+    Q, Cq = mg.merge_pro_360_posed(str(tmp_path), str(out), inv_poses, voxel_size=4.0)
+    # oracle: the written ASCII PLYs (%.4f) read back, posed, merged, filtered
+    parts = [ply.read_ply(str(tmp_path / f"scan_{i:03d}.ply")) for i in range(len(degs))]
+    MP = np.concatenate([o.apply_pose(p, M) for (p, _), M in zip(parts, inv_poses)])
+    MC = np.concatenate([c for _, c in parts])
+    V, VC = mo.voxel_down_sample(MP, MC, 4.0)
+    ind, _ = mo.remove_statistical_outlier(V, 20, 2.0)
+    np.testing.assert_array_equal(Q.cpu().numpy(), V[ind])
+    np.testing.assert_array_equal(Cq.cpu().numpy(), VC[ind])
+    R, RC = ply.read_ply(str(out))
+    np.testing.assert_array_equal(R, V[ind].astype(np.float32).astype(np.float64))
+    np.testing.assert_array_equal(RC, VC[ind])
+    with pytest.raises(ValueError):
+        mg.merge_pro_360_posed(str(tmp_path / "none"), str(out), inv_poses)
