@@ -1,0 +1,96 @@
+"""Merge-stage throughput on a config-5-like cloud.
+
+The workload is V posed 4K views triangulated in one launch (f64 xyz, turntable
+poses), merged in view order.  On it, one JSON line reports:
+
+- ``voxel_down_sample(voxel)``;
+- ``remove_statistical_outlier(20, 2.0)`` on the downsampled cloud.
+
+Both are device time around the blocking calls.  A CPU reference runs beside
+them on a bounded sample, 1 thread: the NumPy voxel oracle, and scipy's
+``cKDTree`` for the kNN means (Open3D is not installed here).
+
+    python scripts/merge_bench.py [--views 4] [--voxel 1.0] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from structured_light_for_3d_model_replication_amd import core, merge, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--views", type=int, default=4)
+    ap.add_argument("--voxel", type=float, default=1.0)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cpu-sample", type=int, default=400_000)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rig = synth.Rig(H=2160, W=3840, Wp=1920, Hp=1080)
+    cal = synth.make_calibration(rig, with_Nc=False)
+    eng = core.Reconstructor(dev)
+    eng.set_calibration(cal, rig.H, rig.W)
+    stack = tex = None
+    poses = torch.empty((a.views, 4, 4), dtype=torch.float64, device=dev)
+    for v in range(a.views):
+        deg = 360.0 * v / a.views
+        s, t = synth.render_stack(rig, seed=500 + v, view_deg=deg, device=dev)
+        if stack is None:
+            stack = torch.empty((a.views,) + tuple(s.shape), dtype=torch.uint8, device=dev)
+            tex = torch.empty((a.views,) + tuple(t.shape), dtype=torch.uint8, device=dev)
+        stack[v].copy_(s)
+        tex[v].copy_(t)
+        poses[v].copy_(torch.from_numpy(synth.turntable_pose(deg)))
+    res = eng.decode_triangulate(stack, texture=tex, xyz_dtype=torch.float64, poses=poses)
+    eng.sync()
+    n = res["cloud"].total()
+    P = res["cloud"].xyz[:n]
+    C = res["cloud"].bgr[:n]
+    del stack, tex
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            out = fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / a.reps, out
+
+    t_vox, (Q, Cq) = timed(lambda: merge.voxel_down_sample(P, C, a.voxel))
+    m = Q.shape[0]
+    t_sor, (ind, _) = timed(lambda: merge.remove_statistical_outlier(Q, 20, 2.0))
+
+    # CPU reference on a bounded sample, 1 thread
+    from scipy.spatial import cKDTree
+
+    from oracle import merge_oracle as mo
+    rng = np.random.default_rng(0)
+    sp = P[torch.from_numpy(rng.choice(n, min(n, a.cpu_sample), replace=False)).to(dev)].cpu().numpy()
+    t0 = time.perf_counter()
+    mo.voxel_down_sample(sp, None, a.voxel)
+    cpu_vox = len(sp) / (time.perf_counter() - t0)
+    sq = Q[: min(m, a.cpu_sample)].cpu().numpy()
+    t0 = time.perf_counter()
+    cKDTree(sq).query(sq, k=20, workers=1)
+    cpu_knn = len(sq) / (time.perf_counter() - t0)
+    print(json.dumps({
+        "workload": f"{a.views} posed 3840x2160 views merged: {n} points (f64), voxel {a.voxel}",
+        "points_in": n, "points_voxel": m, "points_kept": int(ind.shape[0]),
+        "voxel_down_sample_ms": 1e3 * t_vox, "voxel_Mpts_per_s": n / t_vox / 1e6,
+        "statistical_outliers_ms": 1e3 * t_sor, "sor_Mpts_per_s": m / t_sor / 1e6,
+        "cpu_baseline": {"voxel_oracle_Mpts_per_s": cpu_vox / 1e6, "ckdtree_knn20_Mpts_per_s": cpu_knn / 1e6,
+                         "cores": 1, "sample": f"{len(sp)} / {len(sq)} points"},
+    }))
+
+
+if __name__ == "__main__":
+    main()

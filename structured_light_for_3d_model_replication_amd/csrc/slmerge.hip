@@ -23,6 +23,8 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -347,78 +349,306 @@ __device__ __forceinline__ int64_t find_cell(const uint64_t* ukeys, int64_t m, u
   return (a < m && ukeys[a] == key) ? a : -1;
 }
 
+// 21-bit Morton interleave: bit i of x -> bit 3 i (y: 3 i + 1, z: 3 i + 2).
+__host__ __device__ __forceinline__ uint64_t spread3(uint64_t x) {
+  x &= 0x1fffffull;
+  x = (x | (x << 32)) & 0x1f00000000ffffull;
+  x = (x | (x << 16)) & 0x1f0000ff0000ffull;
+  x = (x | (x << 8)) & 0x100f00f00f00f00full;
+  x = (x | (x << 4)) & 0x10c30c30c30c30c3ull;
+  x = (x | (x << 2)) & 0x1249249249249249ull;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint64_t morton3(uint64_t x, uint64_t y, uint64_t z) {
+  return spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
+}
+
+// Morton key of every point's finest cell (h0, origin lo); index = i.
+__global__ __launch_bounds__(kT) void k_morton_keys(const double* xyz, int64_t n, double lo0, double lo1, double lo2,
+                                                    double h, uint64_t* keys, uint32_t* vals) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t ix = static_cast<uint64_t>(floor((xyz[3 * i] - lo0) / h));
+  const uint64_t iy = static_cast<uint64_t>(floor((xyz[3 * i + 1] - lo1) / h));
+  const uint64_t iz = static_cast<uint64_t>(floor((xyz[3 * i + 2] - lo2) / h));
+  keys[i] = morton3(ix, iy, iz);
+  vals[i] = static_cast<uint32_t>(i);
+}
+
+// Level l of the cell pyramid: cells of edge h0 * 2^l = Morton key >> 3 l, each
+// a contiguous run of the Morton-sorted points.
+__global__ __launch_bounds__(kT) void k_heads_shift(const uint64_t* keys, int64_t n, int sh, uint32_t* flag) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i < n) flag[i] = (i == 0 || (keys[i] >> sh) != (keys[i - 1] >> sh)) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kT) void k_level_cells(const uint32_t* flag, const uint32_t* seg, const uint64_t* keys,
+                                                    int64_t n, int sh, uint32_t* starts, uint64_t* ukeys) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i < n && flag[i]) {
+    starts[seg[i]] = static_cast<uint32_t>(i);
+    ukeys[seg[i]] = keys[i] >> sh;
+  }
+}
+
+// Cell of every sorted point: (exclusive scan of the cell heads) + head - 1.
+__global__ __launch_bounds__(kT) void k_cell_of(const uint32_t* flag, const uint32_t* seg, int64_t n, uint32_t* out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i < n) out[i] = seg[i] + flag[i] - 1u;
+}
+
+// Coordinates in Morton order (contiguous candidate runs for the kNN).
+__global__ __launch_bounds__(kT) void k_gather_sorted(const double* xyz, const uint32_t* sidx, int64_t n, double* sxyz) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (t >= n) return;
+  const int64_t i = sidx[t];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) sxyz[3 * t + k] = xyz[3 * i + k];
+}
+
+// The 27 neighbour cells (-1: empty or outside) of every occupied cell of a
+// level, (dx, dy, dz) in -1..1 nesting order.
+__global__ __launch_bounds__(kT) void k_cell_neighbours(const uint64_t* ukeys, int64_t m, int64_t nx, int64_t ny,
+                                                        int64_t nz, int32_t* nbr);
+
+__device__ __forceinline__ uint64_t compact3(uint64_t x) {
+  x &= 0x1249249249249249ull;
+  x = (x | (x >> 2)) & 0x10c30c30c30c30c3ull;
+  x = (x | (x >> 4)) & 0x100f00f00f00f00full;
+  x = (x | (x >> 8)) & 0x1f0000ff0000ffull;
+  x = (x | (x >> 16)) & 0x1f00000000ffffull;
+  x = (x | (x >> 32)) & 0x1fffffull;
+  return x;
+}
+
+__global__ __launch_bounds__(kT) void k_cell_neighbours(const uint64_t* ukeys, int64_t m, int64_t nx, int64_t ny,
+                                                        int64_t nz, int32_t* nbr) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (c >= m) return;
+  const uint64_t key = ukeys[c];
+  const int64_t x = static_cast<int64_t>(compact3(key)), y = static_cast<int64_t>(compact3(key >> 1)),
+                z = static_cast<int64_t>(compact3(key >> 2));
+  int e = 0;
+  for (int dx = -1; dx <= 1; ++dx)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dz = -1; dz <= 1; ++dz, ++e) {
+        const int64_t a = x + dx, b = y + dy, d = z + dz;
+        int64_t f = -1;
+        if (a >= 0 && a < nx && b >= 0 && b < ny && d >= 0 && d < nz) f = find_cell(ukeys, m, morton3(a, b, d));
+        nbr[27 * c + e] = static_cast<int32_t>(f);
+      }
+}
+
+// One candidate squared distance into the sorted k-best list bd (ascending;
+// bd[kk - 1] is the k-th, kept in kth).
+template <int KM>
+__device__ __forceinline__ void knn_take(double (&bd)[KM], double& kth, int64_t& found, int64_t kk, int k, double dd) {
+  ++found;
+  if (dd < kth || found <= kk) {
+    double v = dd;
+#pragma unroll
+    for (int e = 0; e < KM; ++e) {
+      const double lo = fmin(bd[e], v), hi = fmax(bd[e], v);
+      bd[e] = lo;
+      v = hi;
+    }
+    double t2 = bd[KM - 1];
+    if (KM != k || kk != k) {
+      t2 = bd[0];
+#pragma unroll
+      for (int e = 1; e < KM; ++e)
+        if (e == kk - 1) t2 = bd[e];
+    }
+    kth = t2;
+  }
+}
+
+constexpr int kMaxLevels = 22;
+
+struct Pyramid {
+  const uint64_t* ukeys[kMaxLevels];
+  const uint32_t* ustart[kMaxLevels];
+  int64_t m[kMaxLevels];
+  int64_t dim[kMaxLevels][3];  // cells per axis
+  double lo0, lo1, lo2, h0;
+  int l0, levels;
+  unsigned* stats;        // optional: queries finished per level (measurement only)
+  uint32_t* slow_q;       // queries not settled at l0 (sorted positions)
+  unsigned* slow_n;
+  const double* sxyz;     // coordinates in Morton order
+  const uint32_t* cell0;  // level-l0 cell of every sorted point
+  const int32_t* nbr0;    // level-l0 27-neighbour table
+};
+
 // Mean distance to the k nearest points (the point itself included) of every
-// point, in the order of the cell-sorted points (one query per thread).
-__global__ __launch_bounds__(kT) void k_knn_mean(const double* xyz, int64_t n, const uint32_t* sidx,
-                                                 const uint64_t* ukeys, const uint32_t* ustart, int64_t m, Grid g,
+// point; queries in Morton order (one per thread).  From level l0 up: the
+// 3x3x3 cells around the query's cell at level l (every ring at the top
+// level); done once k points are found and the k-th is closer than the
+// searched cube's boundary, else the next coarser level starts over.  KM: the
+// register list length (k itself for the common k = 20, else kMaxK).
+template <int KM>
+__global__ __launch_bounds__(kT) void k_knn_mean(const double* xyz, int64_t n, const uint32_t* sidx, Pyramid py,
                                                  int k, double* avg) {
   const int64_t j = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   if (j >= n) return;
   const int64_t qi = sidx[j];
   const double q0 = xyz[3 * qi], q1 = xyz[3 * qi + 1], q2 = xyz[3 * qi + 2];
-  const int64_t cx = static_cast<int64_t>(floor((q0 - g.lo0) / g.h));
-  const int64_t cy = static_cast<int64_t>(floor((q1 - g.lo1) / g.h));
-  const int64_t cz = static_cast<int64_t>(floor((q2 - g.lo2) / g.h));
-  double bd[kMaxK];
-#pragma unroll
-  for (int e = 0; e < kMaxK; ++e) bd[e] = INFINITY;
-  double kth = INFINITY;  // bd[k - 1]
-  int64_t found = 0;
+  const int64_t fx = static_cast<int64_t>(floor((q0 - py.lo0) / py.h0));
+  const int64_t fy = static_cast<int64_t>(floor((q1 - py.lo1) / py.h0));
+  const int64_t fz = static_cast<int64_t>(floor((q2 - py.lo2) / py.h0));
   const int64_t kk = min<int64_t>(k, n);
-  for (int64_t r = 0;; ++r) {
-    for (int64_t dx = -r; dx <= r; ++dx) {
-      const int64_t x = cx + dx;
-      if (x < 0 || x >= g.nx) continue;
-      for (int64_t dy = -r; dy <= r; ++dy) {
-        const int64_t y = cy + dy;
-        if (y < 0 || y >= g.ny) continue;
-        const bool edge = (dx == -r || dx == r || dy == -r || dy == r);
-        for (int64_t dz = -r; dz <= r; dz += (edge ? 1 : 2 * r > 0 ? 2 * r : 1)) {
-          const int64_t z = cz + dz;
-          if (z < 0 || z >= g.nz) continue;
-          const int64_t c = find_cell(ukeys, m, static_cast<uint64_t>((x * g.ny + y) * g.nz + z));
-          if (c < 0) continue;
-          const int64_t a = ustart[c], b = c + 1 < m ? static_cast<int64_t>(ustart[c + 1]) : n;
-          for (int64_t t = a; t < b; ++t) {
-            const int64_t pi = sidx[t];
-            const double d0 = q0 - xyz[3 * pi], d1 = q1 - xyz[3 * pi + 1], d2 = q2 - xyz[3 * pi + 2];
-            const double dd = ((d0 * d0) + d1 * d1) + d2 * d2;  // nanoflann L2_Adaptor order for 3 dims
-            ++found;
-            if (dd < kth || found <= kk) {
-              double v = dd;
+  const double margin = 1e-12 * (fabs(q0) + fabs(q1) + fabs(q2) + fabs(py.lo0) + fabs(py.lo1) + fabs(py.lo2));
+  double bd[KM];
+  // ---- level l0: the 27 cells of the query's cell from its neighbour table,
+  // candidates read from the Morton-ordered copy, four loads in flight ----
+  {
 #pragma unroll
-              for (int e = 0; e < kMaxK; ++e) {
-                const double lo = fmin(bd[e], v), hi = fmax(bd[e], v);
-                bd[e] = lo;
-                v = hi;
-              }
-              double t2 = bd[0];
+    for (int e = 0; e < KM; ++e) bd[e] = INFINITY;
+    double kth = INFINITY;
+    int64_t found = 0;
+    const int l = py.l0;
+    const uint32_t* us = py.ustart[l];
+    const int64_t m = py.m[l];
+    const int32_t* nb = py.nbr0 + 27 * static_cast<int64_t>(py.cell0[j]);
+    for (int e = 0; e < 27; ++e) {
+      const int64_t c = nb[e];
+      if (c < 0) continue;
+      const int64_t a = us[c], b = c + 1 < m ? static_cast<int64_t>(us[c + 1]) : n;
+      int64_t t = a;
+      for (; t + 4 <= b; t += 4) {
+        double p[12];
 #pragma unroll
-              for (int e = 1; e < kMaxK; ++e)
-                if (e == kk - 1) t2 = bd[e];
-              kth = t2;
+        for (int u = 0; u < 12; ++u) p[u] = py.sxyz[3 * t + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const double d0 = q0 - p[3 * u], d1 = q1 - p[3 * u + 1], d2 = q2 - p[3 * u + 2];
+          knn_take<KM>(bd, kth, found, kk, k, ((d0 * d0) + d1 * d1) + d2 * d2);  // nanoflann L2_Adaptor order
+        }
+      }
+      for (; t < b; ++t) {
+        const double d0 = q0 - py.sxyz[3 * t], d1 = q1 - py.sxyz[3 * t + 1], d2 = q2 - py.sxyz[3 * t + 2];
+        knn_take<KM>(bd, kth, found, kk, k, ((d0 * d0) + d1 * d1) + d2 * d2);
+      }
+    }
+    const double h = ldexp(py.h0, l);
+    const int64_t cx = fx >> l, cy = fy >> l, cz = fz >> l;
+    const int64_t nx = py.dim[l][0], ny = py.dim[l][1], nz = py.dim[l][2];
+    const double lo0 = py.lo0 + static_cast<double>(cx - 1) * h, hi0 = py.lo0 + static_cast<double>(cx + 2) * h;
+    const double lo1 = py.lo1 + static_cast<double>(cy - 1) * h, hi1 = py.lo1 + static_cast<double>(cy + 2) * h;
+    const double lo2 = py.lo2 + static_cast<double>(cz - 1) * h, hi2 = py.lo2 + static_cast<double>(cz + 2) * h;
+    double bound = fmin(fmin(q0 - lo0, hi0 - q0), fmin(fmin(q1 - lo1, hi1 - q1), fmin(q2 - lo2, hi2 - q2)));
+    bound = fmax(bound - margin - 1e-12 * h, 0.0);
+    const bool all = cx - 1 <= 0 && cy - 1 <= 0 && cz - 1 <= 0 && cx + 1 >= nx - 1 && cy + 1 >= ny - 1 &&
+                     cz + 1 >= nz - 1;
+    if (all || (found >= kk && kth < bound * bound)) {
+      if (py.stats) atomicAdd(py.stats + l, 1u);
+      double s = 0.0;
+#pragma unroll
+      for (int e = 0; e < KM; ++e)
+        if (e < kk) s += sqrt(bd[e]);
+      avg[qi] = kk > 0 ? s / static_cast<double>(kk) : -1.0;
+      return;
+    }
+  }
+  // not settled at l0 (an isolated point): to the cooperative kernel
+  py.slow_q[atomicAdd(py.slow_n, 1u)] = static_cast<uint32_t>(j);
+}
+
+// The queries k_knn_mean left, one wave each, from level l0 + 1 up (the top
+// level again, with every ring, when l0 is the top): the lanes split every
+// cell's run of Morton-ordered points, each keeping its own k best; after
+// every ring the 64 lists are merged by k rounds of wave-min selection, which
+// yields the k smallest in ascending order (summed in that order).
+template <int KM>
+__global__ __launch_bounds__(64) void k_knn_slow(const uint32_t* sidx, int64_t n, Pyramid py, int k, double* avg) {
+  const int lane = threadIdx.x;
+  const int64_t j = py.slow_q[blockIdx.x];
+  const int64_t qi = sidx[j];
+  const double q0 = py.sxyz[3 * j], q1 = py.sxyz[3 * j + 1], q2 = py.sxyz[3 * j + 2];
+  const int64_t fx = static_cast<int64_t>(floor((q0 - py.lo0) / py.h0));
+  const int64_t fy = static_cast<int64_t>(floor((q1 - py.lo1) / py.h0));
+  const int64_t fz = static_cast<int64_t>(floor((q2 - py.lo2) / py.h0));
+  const int64_t kk = min<int64_t>(k, n);
+  const double margin = 1e-12 * (fabs(q0) + fabs(q1) + fabs(q2) + fabs(py.lo0) + fabs(py.lo1) + fabs(py.lo2));
+  double bd[KM];
+  for (int l = min(py.l0 + 1, py.levels - 1); l < py.levels; ++l) {
+#pragma unroll
+    for (int e = 0; e < KM; ++e) bd[e] = INFINITY;
+    double kth = INFINITY;
+    int64_t found = 0;
+    const int64_t cx = fx >> l, cy = fy >> l, cz = fz >> l;
+    const int64_t nx = py.dim[l][0], ny = py.dim[l][1], nz = py.dim[l][2];
+    const uint64_t* uk = py.ukeys[l];
+    const uint32_t* us = py.ustart[l];
+    const int64_t m = py.m[l];
+    const bool top = l == py.levels - 1;
+    const double h = ldexp(py.h0, l);
+    for (int64_t r = 0; r <= (top ? (int64_t)1 << 40 : 1); ++r) {
+      for (int64_t dx = -r; dx <= r; ++dx) {
+        const int64_t x = cx + dx;
+        if (x < 0 || x >= nx) continue;
+        for (int64_t dy = -r; dy <= r; ++dy) {
+          const int64_t y = cy + dy;
+          if (y < 0 || y >= ny) continue;
+          const bool edge = (dx == -r || dx == r || dy == -r || dy == r);
+          for (int64_t dz = -r; dz <= r; dz += (edge || r == 0) ? 1 : 2 * r) {
+            const int64_t z = cz + dz;
+            if (z < 0 || z >= nz) continue;
+            const int64_t c = find_cell(uk, m, morton3(x, y, z));
+            if (c < 0) continue;
+            const int64_t a = us[c], b = c + 1 < m ? static_cast<int64_t>(us[c + 1]) : n;
+            for (int64_t t = a + lane; t < b; t += 64) {
+              const double d0 = q0 - py.sxyz[3 * t], d1 = q1 - py.sxyz[3 * t + 1], d2 = q2 - py.sxyz[3 * t + 2];
+              knn_take<KM>(bd, kth, found, kk, k, ((d0 * d0) + d1 * d1) + d2 * d2);  // nanoflann order
             }
           }
         }
       }
-    }
-    // every point outside the searched cube is at least `bound` away
-    const double lo0 = g.lo0 + static_cast<double>(cx - r) * g.h, hi0 = g.lo0 + static_cast<double>(cx + r + 1) * g.h;
-    const double lo1 = g.lo1 + static_cast<double>(cy - r) * g.h, hi1 = g.lo1 + static_cast<double>(cy + r + 1) * g.h;
-    const double lo2 = g.lo2 + static_cast<double>(cz - r) * g.h, hi2 = g.lo2 + static_cast<double>(cz + r + 1) * g.h;
-    double bound = fmin(fmin(q0 - lo0, hi0 - q0), fmin(fmin(q1 - lo1, hi1 - q1), fmin(q2 - lo2, hi2 - q2)));
-    // margin for points filed into a neighbouring cell by the rounding of (p - lo) / h
-    bound -= 1e-12 * (fabs(q0) + fabs(q1) + fabs(q2) + fabs(g.lo0) + fabs(g.lo1) + fabs(g.lo2) + g.h);
-    bound = fmax(bound, 0.0);
-    const bool all = cx - r <= 0 && cy - r <= 0 && cz - r <= 0 && cx + r >= g.nx - 1 && cy + r >= g.ny - 1 &&
-                     cz + r >= g.nz - 1;
-    if (all || (found >= kk && kth < bound * bound)) break;
-  }
-  double s = 0.0;
+      // the wave's k smallest: k rounds of (value, lane) wave-min on the list heads
+      long long fw = found;
 #pragma unroll
-  for (int e = 0; e < kMaxK; ++e)
-    if (e < kk) s += sqrt(bd[e]);
-  avg[qi] = kk > 0 ? s / static_cast<double>(kk) : -1.0;
+      for (int d = 32; d > 0; d >>= 1) fw += __shfl_xor(fw, d, 64);
+      double tmp[KM];
+#pragma unroll
+      for (int e = 0; e < KM; ++e) tmp[e] = bd[e];
+      double kthw = INFINITY, ssum = 0.0;
+      for (int64_t i = 0; i < kk; ++i) {
+        double mv = tmp[0];
+        int ml = lane;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) {
+          const double ov = __shfl_xor(mv, d, 64);
+          const int ol = __shfl_xor(ml, d, 64);
+          if (ov < mv || (ov == mv && ol < ml)) {
+            mv = ov;
+            ml = ol;
+          }
+        }
+        if (lane == ml) {
+#pragma unroll
+          for (int e = 0; e + 1 < KM; ++e) tmp[e] = tmp[e + 1];
+          tmp[KM - 1] = INFINITY;
+        }
+        kthw = mv;
+        ssum += sqrt(mv);
+      }
+      const double lo0 = py.lo0 + static_cast<double>(cx - r) * h, hi0 = py.lo0 + static_cast<double>(cx + r + 1) * h;
+      const double lo1 = py.lo1 + static_cast<double>(cy - r) * h, hi1 = py.lo1 + static_cast<double>(cy + r + 1) * h;
+      const double lo2 = py.lo2 + static_cast<double>(cz - r) * h, hi2 = py.lo2 + static_cast<double>(cz + r + 1) * h;
+      double bound = fmin(fmin(q0 - lo0, hi0 - q0), fmin(fmin(q1 - lo1, hi1 - q1), fmin(q2 - lo2, hi2 - q2)));
+      bound = fmax(bound - margin - 1e-12 * h, 0.0);
+      const bool all = cx - r <= 0 && cy - r <= 0 && cz - r <= 0 && cx + r >= nx - 1 && cy + r >= ny - 1 &&
+                       cz + r >= nz - 1;
+      if (all || (fw >= kk && kthw < bound * bound)) {
+        if (lane == 0) {
+          avg[qi] = kk > 0 ? ssum / static_cast<double>(kk) : -1.0;
+          if (py.stats) atomicAdd(py.stats + kMaxLevels + l, 1u);
+        }
+        return;
+      }
+    }
+  }
 }
 
 __global__ __launch_bounds__(kT) void k_keep_flags(const double* avg, int64_t n, double thr, uint32_t* flag) {
@@ -640,27 +870,128 @@ int sl_statistical_outliers(sl_ctx* c, const double* xyz, int64_t n, int nb_neig
   double b[6];
   int r = bounds(c, xyz, n, b, s);
   if (r) return r;
-  // cell size: about k points per cell for a volume-filling cloud (surfaces
-  // put more per occupied cell); exactness does not depend on it
+  // finest cell: 1/8 of the volume-filling size for ~k points per cell, at
+  // most 2^20 cells per axis; the pyramid doubles it per level
   double ext[3], vol = 1.0, emax = 0.0;
   for (int k = 0; k < 3; ++k) {
     ext[k] = b[3 + k] - b[k];
     emax = std::max(emax, ext[k]);
   }
   for (int k = 0; k < 3; ++k) vol *= std::max(ext[k], emax * 1e-3);
-  double h = cbrt(vol * nb_neighbors / static_cast<double>(n));
-  h = std::max(h, emax / 1.0e6);
-  if (!(h > 0.0) || !std::isfinite(h)) h = 1.0;  // all points coincide (or non-finite input)
-  Grid g;
-  while (!make_grid(b, b + 3, h, &g)) h *= 2.0;
-  DBuf<uint64_t> keys, ukeys;
-  DBuf<uint32_t> idx, ustart;
-  int64_t m = 0;
-  r = cells(c, xyz, n, g, keys, idx, ukeys, ustart, &m, s);
-  if (r) return r;
-  hipLaunchKernelGGL(k_knn_mean, dim3(blocks(n)), dim3(kT), 0, s, xyz, n, idx.p, ukeys.p, ustart.p, m, g,
-                     nb_neighbors, avg_dist);
+  double h0 = cbrt(vol * nb_neighbors / static_cast<double>(n)) / 8.0;
+  h0 = std::max(h0, emax / 1048575.0);
+  if (!(h0 > 0.0) || !std::isfinite(h0)) h0 = 1.0;  // all points coincide (or non-finite input)
+  Pyramid py;
+  memset(&py, 0, sizeof(py));
+  py.lo0 = b[0];
+  py.lo1 = b[1];
+  py.lo2 = b[2];
+  py.h0 = h0;
+  int64_t d0[3];
+  for (int k = 0; k < 3; ++k) {
+    const double e = floor(ext[k] / h0);
+    if (!(e >= 0.0) || e >= 2097151.0) return slgpu_fail(c, SL_EINVAL, "non-finite or degenerate point cloud");
+    d0[k] = static_cast<int64_t>(e) + 1;
+  }
+  DBuf<uint64_t> keys;
+  DBuf<uint32_t> idx, flag, seg;
+  MTRY(c, keys.alloc(n));
+  MTRY(c, idx.alloc(n));
+  MTRY(c, flag.alloc(n));
+  MTRY(c, seg.alloc(n));
+  hipLaunchKernelGGL(k_morton_keys, dim3(blocks(n)), dim3(kT), 0, s, xyz, n, py.lo0, py.lo1, py.lo2, h0, keys.p,
+                     idx.p);
   MTRY(c, hipGetLastError());
+  int bits_axis = 1;
+  while ((int64_t{1} << bits_axis) < std::max(d0[0], std::max(d0[1], d0[2]))) ++bits_axis;
+  r = radix_sort(c, keys.p, idx.p, n, 3 * bits_axis, s);
+  if (r) return r;
+  std::vector<DBuf<uint64_t>> lk(kMaxLevels);
+  std::vector<DBuf<uint32_t>> ls(kMaxLevels);
+  DBuf<uint32_t> cell0;
+  DBuf<int32_t> nbr0;
+  DBuf<double> sxyz;
+  int levels = 0, l0 = -1;
+  for (int l = 0; l < kMaxLevels; ++l) {
+    int64_t ml = 0;
+    hipLaunchKernelGGL(k_heads_shift, dim3(blocks(n)), dim3(kT), 0, s, keys.p, n, 3 * l, flag.p);
+    r = scan_flags(c, flag.p, n, seg.p, &ml, s);
+    if (r) return r;
+    MTRY(c, lk[l].alloc(ml));
+    MTRY(c, ls[l].alloc(ml));
+    hipLaunchKernelGGL(k_level_cells, dim3(blocks(n)), dim3(kT), 0, s, flag.p, seg.p, keys.p, n, 3 * l, ls[l].p,
+                       lk[l].p);
+    MTRY(c, hipGetLastError());
+    py.ukeys[l] = lk[l].p;
+    py.ustart[l] = ls[l].p;
+    py.m[l] = ml;
+    int64_t dmax = 0;
+    for (int k = 0; k < 3; ++k) {
+      py.dim[l][k] = ((d0[k] - 1) >> l) + 1;
+      dmax = std::max(dmax, py.dim[l][k]);
+    }
+    levels = l + 1;
+    // start level: ~k/2 points per occupied cell (or the top)
+    const bool top = dmax <= 4;
+    if (l0 < 0 && (top || 2.0 * static_cast<double>(n) >= static_cast<double>(nb_neighbors) * static_cast<double>(ml))) {
+      l0 = l;
+      MTRY(c, cell0.alloc(n));
+      hipLaunchKernelGGL(k_cell_of, dim3(blocks(n)), dim3(kT), 0, s, flag.p, seg.p, n, cell0.p);
+      MTRY(c, nbr0.alloc(27 * ml));
+      hipLaunchKernelGGL(k_cell_neighbours, dim3(blocks(ml)), dim3(kT), 0, s, lk[l].p, ml, py.dim[l][0],
+                         py.dim[l][1], py.dim[l][2], nbr0.p);
+      MTRY(c, hipGetLastError());
+    }
+    if (top) break;  // a few cells per axis
+  }
+  py.levels = levels;
+  py.l0 = l0;
+  MTRY(c, sxyz.alloc(3 * n));
+  hipLaunchKernelGGL(k_gather_sorted, dim3(blocks(n)), dim3(kT), 0, s, xyz, idx.p, n, sxyz.p);
+  MTRY(c, hipGetLastError());
+  py.sxyz = sxyz.p;
+  py.cell0 = cell0.p;
+  py.nbr0 = nbr0.p;
+  MTRY(c, hipStreamSynchronize(s));
+  DBuf<unsigned> st;
+  const bool want_stats = getenv("SLGPU_MERGE_STATS") != nullptr;
+  if (want_stats) {
+    MTRY(c, st.alloc(2 * kMaxLevels));
+    MTRY(c, hipMemsetAsync(st.p, 0, sizeof(unsigned) * 2 * kMaxLevels, s));
+    py.stats = st.p;
+  }
+  DBuf<uint32_t> slow_q;
+  DBuf<unsigned> slow_n;
+  MTRY(c, slow_q.alloc(n));
+  MTRY(c, slow_n.alloc(1));
+  MTRY(c, hipMemsetAsync(slow_n.p, 0, sizeof(unsigned), s));
+  py.slow_q = slow_q.p;
+  py.slow_n = slow_n.p;
+  if (nb_neighbors == 20)
+    hipLaunchKernelGGL(k_knn_mean<20>, dim3(blocks(n)), dim3(kT), 0, s, xyz, n, idx.p, py, nb_neighbors, avg_dist);
+  else
+    hipLaunchKernelGGL(k_knn_mean<kMaxK>, dim3(blocks(n)), dim3(kT), 0, s, xyz, n, idx.p, py, nb_neighbors,
+                       avg_dist);
+  MTRY(c, hipGetLastError());
+  unsigned n_slow = 0;
+  MTRY(c, hipMemcpyAsync(&n_slow, slow_n.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  MTRY(c, hipStreamSynchronize(s));
+  if (n_slow) {
+    if (nb_neighbors == 20)
+      hipLaunchKernelGGL(k_knn_slow<20>, dim3(n_slow), dim3(64), 0, s, idx.p, n, py, nb_neighbors, avg_dist);
+    else
+      hipLaunchKernelGGL(k_knn_slow<kMaxK>, dim3(n_slow), dim3(64), 0, s, idx.p, n, py, nb_neighbors, avg_dist);
+    MTRY(c, hipGetLastError());
+  }
+  if (want_stats) {
+    unsigned h[2 * kMaxLevels];
+    MTRY(c, hipMemcpyAsync(h, st.p, sizeof(h), hipMemcpyDeviceToHost, s));
+    MTRY(c, hipStreamSynchronize(s));
+    fprintf(stderr, "[slmerge] n=%lld h0=%g l0=%d levels=%d m(l0)=%lld fast-done=%u slow-done:", (long long)n, h0,
+            py.l0, py.levels, (long long)py.m[py.l0], h[py.l0]);
+    for (int l = 0; l < py.levels; ++l) fprintf(stderr, " %u", h[kMaxLevels + l]);
+    fprintf(stderr, "\n");
+  }
   // cloud mean / std of the positive means: sequential, as std::accumulate /
   // std::inner_product in RemoveStatisticalOutliers
   std::vector<double> a(static_cast<size_t>(n));
@@ -678,14 +1009,11 @@ int sl_statistical_outliers(sl_ctx* c, const double* xyz, int64_t n, int nb_neig
   for (double v : a) sq = sq + (v > 0 ? (v - mean) * (v - mean) : 0);
   const double sd = sqrt(sq / static_cast<double>(valid - 1));
   const double thr = mean + std_ratio * sd;
-  DBuf<uint32_t> flag, pos;
-  MTRY(c, flag.alloc(n));
-  MTRY(c, pos.alloc(n));
   hipLaunchKernelGGL(k_keep_flags, dim3(blocks(n)), dim3(kT), 0, s, avg_dist, n, thr, flag.p);
   int64_t kept = 0;
-  r = scan_flags(c, flag.p, n, pos.p, &kept, s);
+  r = scan_flags(c, flag.p, n, seg.p, &kept, s);
   if (r) return r;
-  hipLaunchKernelGGL(k_compact_index, dim3(blocks(n)), dim3(kT), 0, s, flag.p, pos.p, n, out_index);
+  hipLaunchKernelGGL(k_compact_index, dim3(blocks(n)), dim3(kT), 0, s, flag.p, seg.p, n, out_index);
   MTRY(c, hipGetLastError());
   MTRY(c, hipStreamSynchronize(s));
   *out_n = kept;
