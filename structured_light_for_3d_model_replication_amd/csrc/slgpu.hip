@@ -54,6 +54,7 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kPx = 16;                 // pixels per lane in the streaming layout
 constexpr int kChunk = 64 * kPx;        // pixels per wave (one chunk)
+constexpr int kChunkNib = kChunk / 4;   // point-nibble bytes per chunk
 #ifndef SLGPU_RING
 #define SLGPU_RING 48
 #endif
@@ -156,7 +157,7 @@ struct Params {
   double o0, o1, o2;       // Oc
   const double* poses;
   uint16_t* codes;   // [view][HW] records: min(col, Wp-1)
-  uint64_t* ptmask;  // [chunk][16] point bits: bit i of word w = pixel 64 w + i of the chunk
+  uint8_t* ptnib;    // [chunk][4 steps][64 lanes] point nibbles: bit e of byte (s, l) = pixel 256 s + 4 l + e
   int32_t* col_out;
   int32_t* row_out;
   uint8_t* mask_out;
@@ -248,7 +249,7 @@ __device__ __forceinline__ int wave_sum(int s) {
 // ------------------------------------------------------------ thresholds ----
 // np.percentile(black_f32, 95) and max(white - black) of one view
 // (sl_system.py:526-535) from its 256-bin histogram, evaluated by one wave
-// (lane l holds bins 4l..4l+3): numpy 2.x's float32 recipe -- q = f32(95) /
+// (lane l holds bins 4l..4l+3, hmax = 1024 + max(white - black)): numpy 2.x's float32 recipe -- q = f32(95) /
 // f32(100); virtual index (n-1)*q in float32; neighbours floor / floor+1, both
 // clamped to n-1 when the index is >= n-1 (numpy/lib/_function_base_impl.py
 // _get_indexes); gamma = index - floor; _lerp a + (b-a) g, replaced by
@@ -259,9 +260,8 @@ struct Thresholds {
   float noise_floor, dynamic_range;
 };
 
-__device__ Thresholds thresholds_from_hist(const unsigned* h, int64_t n, int lane) {
-  const uint4 b4 = reinterpret_cast<const uint4*>(h)[lane];
-  const int dmax = static_cast<int>(h[256]) - 1024;
+__device__ Thresholds thresholds_from_bins(const uint4 b4, unsigned hmax, int64_t n, int lane) {
+  const int dmax = static_cast<int>(hmax) - 1024;
   const int s4 = static_cast<int>(b4.x + b4.y + b4.z + b4.w);
   const int incl = wave_incl_scan(s4, lane);
   const long long e0 = incl - s4;  // pixels below bin 4 lane
@@ -599,57 +599,65 @@ template <int VEC>
 __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view, int civ, int lane, bool live) {
   const int mode = p.mode;
   const bool vec = VEC > 0;
-  const int64_t HW = p.HW;
-  const int64_t cpx = static_cast<int64_t>(civ) * kChunk;
+  const int HW = static_cast<int>(p.HW);  // < 2^31: one view's stack is < 2 GiB
+  const int cpx = civ * kChunk;
   const int W = p.W;
   const bool codes = (mode & M_CODES) != 0;
   const bool nc = (mode & M_NC) != 0;
+  const uint8_t* vstack = p.stack + view * p.stack_vs;            // wave-uniform bases
+  const uint16_t* vcodes = codes ? p.codes + static_cast<int64_t>(view) * HW : nullptr;
 
-  // ---- loads ----
+  // ---- loads: the view's histogram first (vmcnt is in order: the threshold
+  // scan then waits for it alone), then the chunk ----
+  uint4 hb = make_uint4(0u, 0u, 0u, 0u);
+  unsigned hmax = 0u;
+  const bool adaptive = (mode & M_HIST) && !(p.dbg & 32);
+  if (adaptive) {
+    const unsigned* h = p.hist + view * kSlot;
+    hb = reinterpret_cast<const uint4*>(h)[lane];
+    hmax = h[256];
+  }
   uint32_t wv[4], bv[4];  // 4 pixels per step, one byte each
   uint32_t rc[4][2];      // records: 4 x u16 per step
-  const int64_t px_hi = vec ? HW - 4 : HW - 1;  // clamp for tail loads (keeps 4-pixel alignment)
+  const int px_hi = vec ? HW - 4 : HW - 1;  // clamp for tail loads (keeps 4-pixel alignment)
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int64_t px = min<int64_t>(cpx + 256 * s + 4 * lane, px_hi);
+    const int px = min(cpx + 256 * s + 4 * lane, px_hi);
     if (mode & M_FROMMAPS) {
       wv[s] = bv[s] = 0u;
     } else if (vec) {
-      const uint8_t* sp = p.stack + view * p.stack_vs + px;
-      wv[s] = ld_side4(sp);
-      bv[s] = ld_side4(sp + HW);
+      wv[s] = ld_side4(vstack + px);
+      bv[s] = ld_side4(vstack + HW + px);
     } else {
-      const uint8_t* sp = p.stack + view * p.stack_vs;
       uint32_t a = 0u, b = 0u;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int64_t q = min<int64_t>(px + e, HW - 1);
-        a |= static_cast<uint32_t>(sp[q]) << (8 * e);
-        b |= static_cast<uint32_t>(sp[HW + q]) << (8 * e);
+        const int q = min(px + e, HW - 1);
+        a |= static_cast<uint32_t>(vstack[q]) << (8 * e);
+        b |= static_cast<uint32_t>(vstack[HW + q]) << (8 * e);
       }
       wv[s] = a;
       bv[s] = b;
     }
     if (codes) {
       if (vec) {
-        const uint2 r = ld_side8(p.codes + view * HW + px);
+        const uint2 r = ld_side8(vcodes + px);
         rc[s][0] = r.x;
         rc[s][1] = r.y;
       } else {
-        const uint16_t* rp = p.codes + view * HW;
-        rc[s][0] = rp[min<int64_t>(px, HW - 1)] | (static_cast<uint32_t>(rp[min<int64_t>(px + 1, HW - 1)]) << 16);
-        rc[s][1] = rp[min<int64_t>(px + 2, HW - 1)] | (static_cast<uint32_t>(rp[min<int64_t>(px + 3, HW - 1)]) << 16);
+        rc[s][0] = vcodes[min(px, HW - 1)] | (static_cast<uint32_t>(vcodes[min(px + 1, HW - 1)]) << 16);
+        rc[s][1] = vcodes[min(px + 2, HW - 1)] | (static_cast<uint32_t>(vcodes[min(px + 3, HW - 1)]) << 16);
       }
     }
   }
   uint32_t mk[4] = {0u, 0u, 0u, 0u};  // FROMMAPS: the caller's mask bytes
   if (mode & M_FROMMAPS) {
+    const uint8_t* vm = p.in_mask + static_cast<int64_t>(view) * HW;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int64_t px = cpx + 256 * s + 4 * lane;
+      const int px = cpx + 256 * s + 4 * lane;
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        mk[s] |= (px + e < HW && p.in_mask[view * HW + px + e] != 0) ? (1u << e) : 0u;
+      for (int e = 0; e < 4; ++e) mk[s] |= (px + e < HW && vm[px + e] != 0) ? (1u << e) : 0u;
     }
   }
 
@@ -657,8 +665,8 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
 
   // ---- thresholds (while the loads above are in flight) ----
   int thr_w = 40, thr_c = 10;  // fixed: multi_point_cloud_process.py:36-38
-  if ((mode & M_HIST) && !(p.dbg & 32)) {
-    const Thresholds t = thresholds_from_hist(p.hist + view * kSlot, HW, lane);
+  if (adaptive) {
+    const Thresholds t = thresholds_from_bins(hb, hmax, p.HW, lane);
     thr_w = t.white;
     thr_c = t.contrast;
     if (civ == 0 && lane == 0) {
@@ -670,13 +678,28 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
   }
 
   // ---- mask ----
+  // vec: byte-SWAR in 16-bit lanes (even / odd pixels), two compares per 4
+  // pixels: w > tw  <=>  (0x8000 + w) - (tw + 1) has bit 15, and
+  // w - b > tc  <=>  (0x8000 + w + 16) - (b + tc + 17) has bit 15 -- no borrow
+  // crosses lanes for 0 <= tw + 1 <= 0x7000 and -17 <= tc <= 0x7000 (adaptive:
+  // tw in [0, 382], tc in [-13, 12]).
+  const bool swar = vec && thr_w >= -1 && thr_w < 0x7000 && thr_c >= -17 && thr_c < 0x7000;
+  const uint32_t tw2 = static_cast<uint32_t>(thr_w + 1) * 0x00010001u;
+  const uint32_t tc2 = static_cast<uint32_t>(thr_c + 17) * 0x00010001u;
   uint32_t ok[4];  // bit e: pixel 256 s + 4 lane + e is valid
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    const int64_t px = cpx + 256 * s + 4 * lane;
-    uint32_t m = 0u;
+    const int px = cpx + 256 * s + 4 * lane;
+    uint32_t m = 0u, bytes = 0u;
     if (mode & M_FROMMAPS) {
       m = mk[s];
+    } else if (swar) {
+      const uint32_t we = wv[s] & 0x00ff00ffu, wo = (wv[s] >> 8) & 0x00ff00ffu;
+      const uint32_t be = bv[s] & 0x00ff00ffu, bo = (bv[s] >> 8) & 0x00ff00ffu;
+      const uint32_t me = ((we | 0x80008000u) - tw2) & (((we + 0x00100010u) | 0x80008000u) - (be + tc2));
+      const uint32_t mo = ((wo | 0x80008000u) - tw2) & (((wo + 0x00100010u) | 0x80008000u) - (bo + tc2));
+      bytes = px < HW ? ((me >> 15) & 0x00010001u) | ((mo >> 7) & 0x01000100u) : 0u;
+      m = (bytes & 1u) | ((bytes >> 7) & 2u) | ((bytes >> 14) & 4u) | ((bytes >> 21) & 8u);
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -684,16 +707,17 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
         const int b = static_cast<int>((bv[s] >> (8 * e)) & 0xffu);
         m |= (px + e < HW && w > thr_w && w - b > thr_c) ? (1u << e) : 0u;
       }
+      bytes = (m & 1u) | ((m & 2u) << 7) | ((m & 4u) << 14) | ((m & 8u) << 21);
     }
     ok[s] = m;
     if (mode & M_MAPS) {
-      const uint32_t bytes = (m & 1u) | ((m & 2u) << 7) | ((m & 4u) << 14) | ((m & 8u) << 21);
+      uint8_t* mo_ = p.mask_out + static_cast<int64_t>(view) * HW;
       if (vec) {
-        if (px < HW) *reinterpret_cast<uint32_t*>(p.mask_out + view * HW + px) = bytes;
+        if (px < HW) *reinterpret_cast<uint32_t*>(mo_ + px) = bytes;
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (px + e < HW) p.mask_out[view * HW + px + e] = static_cast<uint8_t>((m >> e) & 1u);
+          if (px + e < HW) mo_[px + e] = static_cast<uint8_t>((m >> e) & 1u);
       }
     }
   }
@@ -702,7 +726,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
   // ---- |n.r| > 1e-6 for the masked pixels ----
   // gathers per step, two steps at a time (the scheduling barrier keeps the
   // second pair's gathers out of the first pair's registers: 4 waves / SIMD)
-  const int u_c = static_cast<int>(cpx % W), v_c = static_cast<int>(cpx / W);  // chunk origin
+  const int v_c = cpx / W, u_c = cpx - v_c * W;  // chunk origin
   int total = 0;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -725,7 +749,10 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
       us = u;
       vs = v;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) pf[e] = p.planes32[(rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu];
+      for (int e = 0; e < 4; ++e) {
+        const unsigned c = (rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu;
+        pf[e] = (p.dbg & 128) ? make_float4(0.5f, 0.25f, 1.0f + 1e-3f * c, 0.0f) : p.planes32[c];
+      }
       ys = 0.0f;
       if (!nc) {
         if (vec) {
@@ -774,12 +801,12 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
           u -= W;
           ++v;
         }
-        const int64_t q = cpx + 256 * s + 4 * lane + e;
+        const int64_t q = static_cast<int64_t>(cpx) + 256 * s + 4 * lane + e;
         float x, y, z, inv;
         if (nc) {
           x = static_cast<float>(p.nc_rays[q]);
-          y = static_cast<float>(p.nc_rays[HW + q]);
-          z = static_cast<float>(p.nc_rays[2 * HW + q]);
+          y = static_cast<float>(p.nc_rays[p.HW + q]);
+          z = static_cast<float>(p.nc_rays[2 * p.HW + q]);
           inv = 1.0f;
         } else {
           x = xs[e];
@@ -791,16 +818,8 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
       }
     }
     total += __popc(nib);
-    // point words of step s: word 4 s + m = the nibbles of lanes 16 m .. 16 m + 15
-    uint32_t lo = (lane & 15) < 8 ? nib << (4 * (lane & 7)) : 0u;
-    uint32_t hi = (lane & 15) >= 8 ? nib << (4 * (lane & 7)) : 0u;
-#pragma unroll
-    for (int d = 1; d < 16; d <<= 1) {
-      lo |= __shfl_xor(lo, d, 64);
-      hi |= __shfl_xor(hi, d, 64);
-    }
-    if ((lane & 15) == 0)
-      p.ptmask[gc * kPx + 4 * s + (lane >> 4)] = static_cast<uint64_t>(lo) | (static_cast<uint64_t>(hi) << 32);
+    // point nibble of (step s, lane): one byte, pixel order within the chunk
+    p.ptnib[gc * kChunkNib + 64 * s + lane] = static_cast<uint8_t>(nib);
   }
   total = wave_sum(total);
   if (lane == 0) p.chunk_counts[gc] = total;
@@ -913,9 +932,10 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
     tq[0] = ld16(p.stack + view * p.stack_vs + pxl, n_px, vec);
     tq[1] = tq[2] = make_uint4(0u, 0u, 0u, 0u);
   }
-  // the lane's 16 point bits (k_count): bits [16 l, 16 l + 16) of the chunk's mask
-  const uint32_t ptbits =
-      static_cast<uint32_t>(p.ptmask[gc * kPx + (lane >> 2)] >> (16 * (lane & 3))) & 0xffffu;
+  // the lane's 16 point bits (k_count): the nibbles of pixels 16 l .. 16 l + 15,
+  // bytes 64 (l / 16) + 4 (l % 16) + 0..3 of the chunk
+  const uint32_t nb4 = *reinterpret_cast<const uint32_t*>(p.ptnib + gc * kChunkNib + 64 * (lane >> 4) + 4 * (lane & 15));
+  const uint32_t ptbits = (nb4 & 0xfu) | ((nb4 >> 4) & 0xf0u) | ((nb4 >> 8) & 0xf00u) | ((nb4 >> 12) & 0xf000u);
   const int n_l = __popc(ptbits);
   const int incl = wave_incl_scan(n_l, lane);
   const int total = __shfl(incl, 63, 64);
@@ -1232,8 +1252,8 @@ struct sl_ctx {
   int64_t cap_cc = 0;
   int* d_block_sums = nullptr;
   int64_t cap_bs = 0;
-  uint64_t* d_ptmask = nullptr;
-  int64_t cap_ptmask = 0;
+  uint8_t* d_ptnib = nullptr;
+  int64_t cap_ptnib = 0;
   uint16_t* d_codes = nullptr;  // k_decode -> k_count / k_cloud records
   int64_t cap_codes = 0;
   int last_views = 0;
@@ -1283,7 +1303,7 @@ int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes) {
   if (r) return r;
   r = grow(c, &c->d_block_sums, &c->cap_bs, views * (((px + kChunk - 1) / kChunk + kWaves - 1) / kWaves));
   if (r) return r;
-  r = grow(c, &c->d_ptmask, &c->cap_ptmask, chunks * kPx);
+  r = grow(c, &c->d_ptnib, &c->cap_ptnib, chunks * kChunkNib);
   if (r) return r;
   for (int b = 0; b < 2; ++b) {
     const int64_t before = c->cap_hist[b];
@@ -1361,7 +1381,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     p.base_in = (v0 > 0 && p.view_offsets) ? p.view_offsets : nullptr;
     p.stats = c->d_stats + v0;
     p.codes = c->d_codes;
-    p.ptmask = c->d_ptmask;
+    p.ptnib = c->d_ptnib;
     p.chunk_counts = c->d_chunk_counts;
     p.block_sums = c->d_block_sums;
     if (adaptive) {
@@ -1545,7 +1565,7 @@ void sl_ctx_destroy(sl_ctx* c) {
   for (void* ptr : {static_cast<void*>(c->d_planes), static_cast<void*>(c->d_xn), static_cast<void*>(c->d_yn),
                     static_cast<void*>(c->d_nc), static_cast<void*>(c->d_stats), static_cast<void*>(c->d_f32),
                     static_cast<void*>(c->d_codes), static_cast<void*>(c->d_hist[0]),
-                    static_cast<void*>(c->d_hist[1]), static_cast<void*>(c->d_ptmask),
+                    static_cast<void*>(c->d_hist[1]), static_cast<void*>(c->d_ptnib),
                     static_cast<void*>(c->d_block_sums), static_cast<void*>(c->d_chunk_counts)})
     if (ptr) (void)hipFree(ptr);
   delete c;
