@@ -880,11 +880,15 @@ constexpr bool kStageOut = SLGPU_STAGE_OUT != 0;  // f32 points leave through an
 #endif
 constexpr bool kLdsBgr = SLGPU_LDS_BGR != 0;  // compacted colours in LDS (else re-read from the texture)
 
+template <int MODE>
+__device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
+                                             int total, const uint32_t* s_ent, const uint32_t* s_bgr,
+                                             float* s_sxyz, uint8_t* s_scol);
+
 // One chunk (global index gc, output offset base) of k_cloud, by one wave.
 template <int MODE, int VEC>
 __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane,
                                             uint32_t* s_ent, uint32_t* s_bgr, float* s_sxyz, uint8_t* s_scol) {
-  const int mode = MODE >= 0 ? MODE : p.mode;
   const bool vec = VEC > 0;
   const int view = static_cast<int>(gc / p.cpv);
   const int civ = static_cast<int>(gc - static_cast<int64_t>(view) * p.cpv);
@@ -969,7 +973,18 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   __builtin_amdgcn_wave_barrier();
   if (p.dbg & 16) return;  // measurement only: stop after the LDS compaction
 
-  // ---- 3. points ----
+  cloud_points<MODE>(p, view, cpx, base, lane, total, s_ent, s_bgr, s_sxyz, s_scol);
+}
+
+// Phase 3 of a chunk: its `total` compacted points (s_ent: pixel | code << 10,
+// s_bgr: colour) -> xyz + BGR at offset base + rank, kPipe x 64 per pass.
+template <int MODE>
+__device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
+                                             int total, const uint32_t* s_ent, const uint32_t* s_bgr,
+                                             float* s_sxyz, uint8_t* s_scol) {
+  const int mode = MODE >= 0 ? MODE : p.mode;
+  const int64_t HW = p.HW;
+  const bool has_tex = p.tex != nullptr;
   // r = (x, y, 1) / sqrt((x*x + y*y) + 1) (sl_system.py:614-621) or Nc
   // (:605-606), plane of the clipped code (:624-633), den = (n0 r0 + n1 r1) +
   // n2 r2 (:638), t = -(n.Oc + d) / den (:639, :643; n.Oc + d per plane,
