@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import glob
 import os
+import threading
 
 import numpy as np
 from PIL import Image
@@ -53,6 +54,54 @@ def imread_bgr(path: str) -> np.ndarray:
             a = np.asarray(im)
             return np.repeat(a[:, :, None], 3, axis=2)
         return np.ascontiguousarray(np.asarray(im.convert("RGB"))[:, :, ::-1])
+
+
+def frame_size(path: str) -> tuple[int, int]:
+    """(H, W) of an image file, from its header only."""
+    with Image.open(path) as im:
+        return im.size[1], im.size[0]
+
+
+_POOL = None
+_POOL_LOCK = threading.Lock()
+
+
+def _pool(workers: int):
+    global _POOL
+    from concurrent.futures import ThreadPoolExecutor
+    with _POOL_LOCK:
+        if _POOL is None or _POOL._max_workers < workers:
+            _POOL = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="sl-ingest")
+        return _POOL
+
+
+def fill_stack(files: list[str], stack_out, tex_out, workers: int = 8) -> bool:
+    """Decode files[0 : len(stack_out)] as gray straight into ``stack_out``
+    (uint8 [n, H, W], e.g. a pinned tensor's numpy view) and file 0 in colour
+    into ``tex_out`` [H, W, 3] BGR -- unless file 0 is single-channel, whose
+    colour read is the gray plane replicated (cv2.imread): then ``tex_out`` is
+    left untouched and True is returned (the caller may pass no texture)."""
+    n = len(stack_out)
+    if len(files) < n:
+        raise ValueError(f"{len(files)} files for {n} planes")
+    shape = tuple(stack_out.shape[1:])
+
+    def one(j):
+        a = imread_gray(files[j])
+        if a.shape != shape:
+            raise ValueError(f"{files[j]}: size {a.shape} differs from {shape}")
+        stack_out[j] = a
+
+    if workers > 1 and n > 1:
+        list(_pool(workers).map(one, range(n)))
+    else:
+        for j in range(n):
+            one(j)
+    with Image.open(files[0]) as im:
+        gray = im.mode == "L"
+    if not gray:
+        tex_out[...] = imread_bgr(files[0])
+    return gray
 
 
 def read_stack(folder: str, workers: int = 8):

@@ -16,7 +16,7 @@ import numpy as np
 import scipy.io
 import torch
 
-from . import core, io, ply
+from . import core, io, pipeline, ply
 from .sl_system import reconstruct_point_cloud  # identical arithmetic (:73-119)
 
 __all__ = ["load_calibration", "gray_decode", "reconstruct_point_cloud", "save_ply", "process_single",
@@ -59,11 +59,19 @@ def process_single(scan_dir, calib_data, *, device=None, log=print):
     return out_path
 
 
-def process_batch(parent_dir, calib_data, *, n_cols=1920, n_rows=1080, device=None, write=True, log=print):
+def process_batch(parent_dir, calib_data, *, n_cols=1920, n_rows=1080, device=None, write=True, log=print,
+                  streamed=True, slots=3, keep=True):
     """Batch mode of multi_point_cloud_process.py:241-257: every subfolder with
-    images is one view.  Views of equal size are decoded + triangulated in ONE
-    fused GPU launch (merged cloud, per-view offsets); per-view PLY files are
-    written exactly as the reference writes them.  Returns {folder: (P, C)}."""
+    images is one view; per-view PLY files are written exactly as the
+    reference writes them.  Returns {folder: (P, C)} (empty lists when
+    ``keep`` is False: a long scan then holds only ``slots`` views in memory).
+
+    ``streamed`` (default): views of equal frame size and file count go
+    through a ``pipeline.ViewPipeline`` -- file decoding of view i+2, H2D of
+    view i+1, the kernels of view i and D2H + PLY writing of view i-1 overlap,
+    and only the planes the cloud reads are decoded and uploaded.  Otherwise
+    all stacks are read first and decoded + triangulated in ONE fused GPU
+    launch (merged cloud, per-view offsets)."""
     subfolders = sorted(f.path for f in os.scandir(parent_dir) if f.is_dir())
     views = [f for f in subfolders if io.list_stack_files(f)]
     for f in subfolders:
@@ -71,6 +79,8 @@ def process_batch(parent_dir, calib_data, *, n_cols=1920, n_rows=1080, device=No
             log(f"Skipping {os.path.basename(f)} (No images found).")
     if not views:
         return {}
+    if streamed:
+        return _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slots, keep)
     stacks, texes = [], []
     for f in views:
         st, tex, _ = io.read_stack(f)
@@ -98,3 +108,47 @@ def process_batch(parent_dir, calib_data, *, n_cols=1920, n_rows=1080, device=No
             save_ply(P, C, os.path.join(f, os.path.basename(f) + ".ply"))
             log(f"Saved: {os.path.basename(f)}.ply ({len(P)} points)")
     return out
+
+
+def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slots, keep):
+    files = {f: io.list_stack_files(f) for f in views}
+    groups: dict = {}
+    for f in views:
+        groups.setdefault((io.frame_size(files[f][0]), len(files[f])), []).append(f)
+    eng = core.engine(device)
+    out = {}
+    failed = set()
+
+    def error(f, e):  # the batch loop's per-folder handler (multi_point_cloud_process.py:248-251)
+        failed.add(f)
+        log(f"❌ Error in {os.path.basename(f)}: {e}\n")
+
+    for ((H, W), n_img), group in groups.items():
+        try:
+            eng.set_calibration(calib_data, H, W)
+            pipe = pipeline.ViewPipeline(eng, H=H, W=W, n_img=n_img, n_cols=n_cols, n_rows=n_rows,
+                                         mask_mode="fixed", xyz_dtype=torch.float64, slots=slots)
+        except (ValueError, IndexError) as e:
+            for f in group:
+                error(f, e)
+            continue
+
+        def fill(i, stack, tex, group=group):
+            try:
+                return io.fill_stack(files[group[i]], stack.numpy(), tex.numpy())
+            except (OSError, ValueError) as e:
+                error(group[i], e)
+                stack[0].zero_()  # white = 0: every pixel masked out, no points
+                return True
+
+        def consume(i, xyz, bgr, group=group):
+            f = group[i]
+            if f in failed:
+                return
+            if write:
+                save_ply(xyz, bgr, os.path.join(f, os.path.basename(f) + ".ply"))
+                log(f"Saved: {os.path.basename(f)}.ply ({len(xyz)} points)")
+            out[f] = (xyz.copy(), bgr.copy()) if keep else ([], [])
+
+        pipe.run(len(group), fill, consume)
+    return {f: out[f] for f in views if f in out}
