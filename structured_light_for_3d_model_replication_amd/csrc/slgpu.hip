@@ -153,6 +153,7 @@ struct Params {
   const double* yn;        // (v - cy) / fy
   const float* xn32;
   const float* yn32;
+  float fast_thr;          // k_count's one-compare sufficient |n.r| test (sl_set_calib)
   const double* nc_rays;   // Nc table [3][HW] or null
   double o0, o1, o2;       // Oc
   const double* poses;
@@ -769,31 +770,31 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
       }
     }
     uint32_t nib = 0u;
+    // Cheap sufficient test (pinhole rays): with L = |x| + |y| + 1 >= |(x, y, 1)|
+    // and a = |n.(x, y, 1)| in f32 (error < sum|n_i| L 2^-20, the inputs' f32
+    // rounding included), a > L (1.001e-6 + sum|n_i| 2^-20) implies |n.r| >
+    // 1.001e-6 for the exact ray, clear of the reference's f64 rounding.
+    // p.fast_thr is that right-hand side at the frame's largest L and the
+    // table's largest sum|n_i| (sl_set_calib, rounded up): one compare per
+    // pixel.  Masked pixels that fail it take the bounded test below.
+    uint32_t todo = ok[s];
+    if (p.dbg & 64) {
+      nib = todo;
+      todo = 0u;
+    } else if (vec && !nc) {
+      uint32_t fast = 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float4 f = pf[e];
+        const float a = fabsf(__builtin_fmaf(f.x, xs[e], __builtin_fmaf(f.y, ys, f.z)));
+        fast |= (a > p.fast_thr) ? (1u << e) : 0u;
+      }
+      nib = todo & fast;
+      todo &= ~fast;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      if (!((ok[s] >> e) & 1u)) continue;
-      if (p.dbg & 64) {
-        nib |= 1u << e;
-        continue;
-      }
-      if (!nc) {
-        // Cheap sufficient test: with L = |x| + |y| + 1 >= |(x, y, 1)| and
-        // a = |n.(x, y, 1)| in f32 (error < sum|n_i| L 2^-20, inputs' f32
-        // rounding included), a > L (1.001e-6 + sum|n_i| 2^-20) implies
-        // |n.r| > 1.001e-6 for the exact ray, clear of the reference's f64
-        // rounding.  Pixels that fail take the bounded test below.
-        const float4 f = pf[e];
-        const float x = xs[e], y = vec ? ys : 0.0f;
-        if (vec) {
-          const float a = fabsf(f.x * x + f.y * y + f.z);
-          const float L = fabsf(x) + fabsf(y) + 1.0f;
-          const float nsum = fabsf(f.x) + fabsf(f.y) + fabsf(f.z);
-          if (a > L * (1.001e-6f + nsum * 9.5367431640625e-07f)) {
-            nib |= 1u << e;
-            continue;
-          }
-        }
-      }
+      if (!((todo >> e) & 1u)) continue;
       {
         const int c = static_cast<int>((rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu);
         int u = us + e, v = vs;
@@ -1255,6 +1256,7 @@ struct sl_ctx {
   double* d_xn = nullptr;
   double* d_yn = nullptr;
   float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H]
+  float fast_thr = 0.0f;   // k_count's sufficient |n.r| threshold (Params::fast_thr)
   double* d_nc = nullptr;
   // scratch
   ViewStats* d_stats = nullptr;
@@ -1648,6 +1650,19 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
     for (int i = 0; i < 4 * Wp; ++i) f[i] = static_cast<float>(pl[i]);  // w: f32 of n.Oc + d
     for (int u = 0; u < W; ++u) f[4 * Wp + u] = static_cast<float>(xn[u]);
     for (int v = 0; v < H; ++v) f[4 * Wp + W + v] = static_cast<float>(yn[v]);
+    // k_count's one-compare test: L (1.001e-6 + sum|n_i| 2^-20) at the largest
+    // L = |x| + |y| + 1 of the frame and the largest sum|n_i| of the table
+    // (of the f32 values the kernel reads), in f64, rounded up to f32
+    double xm = 0.0, ym = 0.0, nm = 0.0;
+    for (int u = 0; u < W; ++u) xm = std::max(xm, fabs(static_cast<double>(f[4 * Wp + u])));
+    for (int v = 0; v < H; ++v) ym = std::max(ym, fabs(static_cast<double>(f[4 * Wp + W + v])));
+    for (int i = 0; i < Wp; ++i)
+      nm = std::max(nm, (fabs(static_cast<double>(f[4 * i])) + fabs(static_cast<double>(f[4 * i + 1]))) +
+                            fabs(static_cast<double>(f[4 * i + 2])));
+    const double thr = ((xm + ym) + 1.0) * (1.001e-6 + nm * 9.5367431640625e-07);
+    float thr32 = static_cast<float>(thr);
+    if (static_cast<double>(thr32) < thr) thr32 = nextafterf(thr32, INFINITY);
+    c->fast_thr = std::isfinite(thr32) ? thr32 : INFINITY;
     HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_f32), sizeof(float) * f.size()));
     HIP_TRY(c, hipMemcpy(c->d_f32, f.data(), sizeof(float) * f.size(), hipMemcpyHostToDevice));
   }
@@ -1706,6 +1721,7 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.planes32 = reinterpret_cast<const float4*>(c->d_f32);
   p.xn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp : nullptr;
   p.yn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp + c->W : nullptr;
+  p.fast_thr = c->fast_thr;
   p.nc_rays = c->d_nc;
   p.o0 = c->Oc[0];
   p.o1 = c->Oc[1];
