@@ -109,10 +109,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # launched by torch.distributed.run (any world size, 1 included): RCCL process
+    # group, barrier + max-over-ranks timing and the gather all run
+    distributed = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
+    if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", local if distributed else 0)
     torch.cuda.set_device(dev)
     cfg = CONFIGS[a.config]
     H, W, Wp, Hp, rows, maps = cfg["H"], cfg["W"], cfg["Wp"], cfg["Hp"], cfg["rows"], cfg["maps"]
@@ -155,18 +158,18 @@ def main():
         step(out)
     eng.sync()
     n_pts = int(out["view_offsets"][-1].item())
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step(out)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
+    if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
 
@@ -215,7 +218,7 @@ def main():
         del out3
 
     gather_ms = None
-    if world > 1:
+    if distributed:
         n_loc = int(out["view_offsets"][-1].item())
         dist.barrier()
         torch.cuda.synchronize(dev)
@@ -286,7 +289,7 @@ def main():
             "alt_xyz_mode": alt,
         }
         print(json.dumps(res))
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 
