@@ -198,6 +198,20 @@ int sl_select_by_index(sl_ctx* ctx, const double* xyz, const uint8_t* bgr, const
  * ((m0 x + m1 y) + m2 z) + m3 -- PointCloud::Transform.  Asynchronous. */
 int sl_transform_points(sl_ctx* ctx, double* xyz, int64_t n, const double* pose, void* stream);
 
+/* ---- calibration products (csrc/slcalib.hip) ----
+ * Replaces the NumPy tail of SLSystem.calibrate_final (server/sl_system.py:348-403):
+ * from the stereo parameters OpenCV estimated (cam_K = K1, proj_K = K2, R, T;
+ * row-major 3x3 / 3) it derives, on the device,
+ *   nc_out        [3][cam_h*cam_w]  unit camera rays, pixel v*cam_w + u (Nc, :353-365)
+ *   plane_col_out [4][proj_w]       column planes (n0, n1, n2, d) (wPlaneCol as saved, :397-398, :408)
+ *   plane_row_out [4][proj_h]       row planes (wPlaneRow, :401-402, :409)
+ * (any output may be NULL; proj_w x proj_h = SCREEN_WIDTH x SCREEN_HEIGHT of
+ * config.py).  Bit-identical to the reference's NumPy 2.2 / OpenBLAS 0.3.29
+ * evaluation (3-term dots as left-to-right FMA chains).  Asynchronous. */
+int sl_calib_products(sl_ctx* ctx, const double* cam_K, const double* proj_K, const double* R, const double* T,
+                      int cam_w, int cam_h, int proj_w, int proj_h, double* nc_out, double* plane_col_out,
+                      double* plane_row_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

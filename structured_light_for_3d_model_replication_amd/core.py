@@ -243,6 +243,28 @@ class Reconstructor:
                 self._ctx, "sl_triangulate_maps")
         return Cloud(xyz, bgr, vo)
 
+    def calib_products(self, cam_K, proj_K, R, T, cam_w: int, cam_h: int, proj_w: int = 1920,
+                       proj_h: int = 1080, rays: bool = True, stream=None):
+        """Calibration products of calibrate_final (sl_system.py:348-403) on the
+        device (csrc/slcalib.hip): -> (Nc [3, cam_h*cam_w] or None,
+        wPlaneCol [4, proj_w], wPlaneRow [4, proj_h]) float64 tensors."""
+        K1 = _f64c(cam_K).reshape(3, 3)
+        K2 = _f64c(proj_K).reshape(3, 3)
+        Rm = _f64c(R).reshape(3, 3)
+        Tv = _f64c(T).reshape(-1)
+        if Tv.size != 3:
+            raise ValueError("T must have 3 entries")
+        f64 = dict(dtype=torch.float64, device=self.device)
+        nc = torch.empty((3, int(cam_h) * int(cam_w)), **f64) if rays else None
+        col = torch.empty((4, int(proj_w)), **f64)
+        row = torch.empty((4, int(proj_h)), **f64)
+        with self._lock:
+            _lib.check(self._L.sl_calib_products(self._ctx, K1.ctypes.data, K2.ctypes.data, Rm.ctypes.data,
+                                                 Tv.ctypes.data, int(cam_w), int(cam_h), int(proj_w),
+                                                 int(proj_h), _ptr(nc), col.data_ptr(), row.data_ptr(),
+                                                 self._stream(stream)), self._ctx, "sl_calib_products")
+        return nc, col, row
+
     def sync(self, stream=None) -> None:
         """Wait for this context's work and raise on device-side failures."""
         with self._lock:
