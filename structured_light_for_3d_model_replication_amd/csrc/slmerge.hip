@@ -479,6 +479,7 @@ struct Pyramid {
   const double* sxyz;     // coordinates in Morton order
   const uint32_t* cell0;  // level-l0 cell of every sorted point
   const int32_t* nbr0;    // level-l0 27-neighbour table
+  const uint32_t* fchild[kMaxLevels];  // levels > l0: first child of every cell (+ sentinel)
 };
 
 // Mean distance to the k nearest points (the point itself included) of every
@@ -649,6 +650,177 @@ __global__ __launch_bounds__(64) void k_knn_slow(const uint32_t* sidx, int64_t n
       }
     }
   }
+}
+
+// First child (at level l - 1) of every cell of level l >= 1, plus a sentinel
+// fc[m_l] = m_{l-1}: the children of cell c are fc[c] .. fc[c + 1] - 1 (a
+// parent's children are the consecutive cells whose key >> 3 is its key).
+__global__ __launch_bounds__(kT) void k_first_child(const uint64_t* ukeys, int64_t m, const uint64_t* ckeys,
+                                                    int64_t mc, uint32_t* fc) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (c > m) return;
+  if (c == m) {
+    fc[m] = static_cast<uint32_t>(mc);
+    return;
+  }
+  const uint64_t key = ukeys[c] << 3;
+  int64_t a = 0, b = mc;  // first child key >= key
+  while (a < b) {
+    const int64_t h = (a + b) >> 1;
+    if (ckeys[h] < key) a = h + 1;
+    else b = h;
+  }
+  fc[c] = static_cast<uint32_t>(a);
+}
+
+constexpr int kBestCap = 4096;  // frontier cells per query (LDS)
+
+// Squared distance from q to the box of cell (x, y, z) of edge h, lowered by a
+// relative margin far above the rounding of point -> cell assignment and of
+// the squared sums: a lower bound of every member point's computed distance.
+__device__ __forceinline__ double cell_mind2(const Pyramid& py, uint64_t key, double h, double q0, double q1,
+                                             double q2) {
+  const double x = static_cast<double>(compact3(key)), y = static_cast<double>(compact3(key >> 1)),
+               z = static_cast<double>(compact3(key >> 2));
+  auto gap = [&](double lo, double c, double q) {
+    const double a = lo + c * h, b = lo + (c + 1.0) * h;
+    const double marg = 1e-12 * (fabs(a) + fabs(b) + fabs(q) + fabs(lo)) + 1e-12 * h;
+    return fmax(fmax(a - q, q - b) - marg, 0.0);
+  };
+  const double g0 = gap(py.lo0, x, q0), g1 = gap(py.lo1, y, q1), g2 = gap(py.lo2, z, q2);
+  return ((g0 * g0 + g1 * g1) + g2 * g2) * (1.0 - 1e-12);
+}
+
+// The queries k_knn_mean left (isolated points), one wave each: best-first
+// search of the cell pyramid.  The frontier (cells with a lower bound of their
+// points' distances) lives in LDS; each step pops the nearest cell -- its
+// children are pushed, or, at the start level, its points are scanned -- until
+// the nearest frontier cell is no closer than the k-th best distance.  The k
+// best squared distances are one sorted list across the wave (lane i holds the
+// i-th smallest): a candidate below the k-th is inserted by one shift.  The
+// result is the same multiset of k smallest distances as the exhaustive
+// search, so the mean (ascending square roots) is bit-identical.  Frontier
+// overflow (more than kBestCap cells) hands the query to k_knn_slow.
+template <int KM>
+__global__ __launch_bounds__(64) void k_knn_best(const uint32_t* sidx, int64_t n, Pyramid py, int k, double* avg,
+                                                 uint32_t* over_q, unsigned* over_n) {
+  __shared__ double f_key[kBestCap];
+  __shared__ uint32_t f_cell[kBestCap];
+  __shared__ uint8_t f_lev[kBestCap];
+  __shared__ int f_n;
+  const int lane = threadIdx.x;
+  const int64_t j = py.slow_q[blockIdx.x];
+  const int64_t qi = sidx[j];
+  const double q0 = py.sxyz[3 * j], q1 = py.sxyz[3 * j + 1], q2 = py.sxyz[3 * j + 2];
+  const int kk = static_cast<int>(min<int64_t>(k, n));
+  const int top = py.levels - 1;
+  // frontier: every cell of the top level (at most 4 x 4 x 4)
+  if (lane == 0) f_n = 0;
+  __syncthreads();
+  {
+    const double h = ldexp(py.h0, top);
+    for (int64_t c = lane; c < py.m[top]; c += 64) {
+      const int at = atomicAdd(&f_n, 1);
+      f_key[at] = cell_mind2(py, py.ukeys[top][c], h, q0, q1, q2);
+      f_cell[at] = static_cast<uint32_t>(c);
+      f_lev[at] = static_cast<uint8_t>(top);
+    }
+  }
+  __syncthreads();
+  double lv = INFINITY;  // the wave's sorted k-best list, entry `lane`
+  bool overflow = false;
+  for (;;) {
+    const int fn = f_n;
+    if (fn == 0) break;
+    // nearest frontier cell (lowest index on ties)
+    double mk = INFINITY;
+    int mi = 0x7fffffff;
+    for (int e = lane; e < fn; e += 64)
+      if (f_key[e] < mk) {
+        mk = f_key[e];
+        mi = e;
+      }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      const double ok_ = __shfl_xor(mk, d, 64);
+      const int oi = __shfl_xor(mi, d, 64);
+      if (ok_ < mk || (ok_ == mk && oi < mi)) {
+        mk = ok_;
+        mi = oi;
+      }
+    }
+    const double kth = __shfl(lv, kk - 1, 64);
+    if (mk >= kth) break;  // no frontier cell can hold a point closer than the k-th
+    const int64_t cell = f_cell[mi];
+    const int l = f_lev[mi];
+    __syncthreads();
+    if (lane == 0) {  // remove mi: the last entry takes its place
+      f_key[mi] = f_key[fn - 1];
+      f_cell[mi] = f_cell[fn - 1];
+      f_lev[mi] = f_lev[fn - 1];
+      f_n = fn - 1;
+    }
+    __syncthreads();
+    if (l <= py.l0) {
+      // leaf: the cell's Morton-ordered points, 64 per batch
+      const int64_t m = py.m[l];
+      const int64_t a = py.ustart[l][cell], b = cell + 1 < m ? static_cast<int64_t>(py.ustart[l][cell + 1]) : n;
+      for (int64_t t0 = a; t0 < b; t0 += 64) {
+        const int64_t t = t0 + lane;
+        double dd = INFINITY;
+        if (t < b) {
+          const double d0 = q0 - py.sxyz[3 * t], d1 = q1 - py.sxyz[3 * t + 1], d2 = q2 - py.sxyz[3 * t + 2];
+          dd = ((d0 * d0) + d1 * d1) + d2 * d2;  // nanoflann L2_Adaptor order
+        }
+        double kcur = __shfl(lv, kk - 1, 64);
+        uint64_t want = __ballot(t < b && dd < kcur);
+        while (want) {
+          const int src = __builtin_ctzll(want);
+          want &= want - 1;
+          const double v = __shfl(dd, src, 64);
+          if (!(v < kcur)) continue;
+          const double up = __shfl_up(lv, 1, 64);
+          if (lane < kk && !(lv <= v)) lv = (lane == 0 || up <= v) ? v : up;
+          kcur = __shfl(lv, kk - 1, 64);
+        }
+      }
+    } else {
+      // inner cell: push the children whose bound is below the k-th
+      const uint32_t* fcl = py.fchild[l];
+      const int64_t c0 = fcl[cell], c1 = fcl[cell + 1];
+      const double h = ldexp(py.h0, l - 1);
+      const double kcur = __shfl(lv, kk - 1, 64);
+      bool push = false;
+      double key2 = 0.0;
+      if (lane < c1 - c0) {
+        key2 = cell_mind2(py, py.ukeys[l - 1][c0 + lane], h, q0, q1, q2);
+        push = key2 < kcur;
+      }
+      const uint64_t pm = __ballot(push);
+      const int np = __popcll(pm);
+      if (fn - 1 + np > kBestCap) {
+        overflow = true;
+        break;
+      }
+      if (push) {
+        const int at = fn - 1 + __popcll(pm & ((1ull << lane) - 1ull));
+        f_key[at] = key2;
+        f_cell[at] = static_cast<uint32_t>(c0 + lane);
+        f_lev[at] = static_cast<uint8_t>(l - 1);
+      }
+      __syncthreads();
+      if (lane == 0) f_n = fn - 1 + np;
+      __syncthreads();
+    }
+  }
+  if (overflow) {
+    if (lane == 0) over_q[atomicAdd(over_n, 1u)] = static_cast<uint32_t>(j);
+    return;
+  }
+  // mean of the k square roots, ascending (the list order)
+  double s = 0.0;
+  for (int e = 0; e < kk; ++e) s += sqrt(__shfl(lv, e, 64));
+  if (lane == 0) avg[qi] = kk > 0 ? s / static_cast<double>(kk) : -1.0;
 }
 
 __global__ __launch_bounds__(kT) void k_keep_flags(const double* avg, int64_t n, double thr, uint32_t* flag) {
@@ -946,6 +1118,15 @@ int sl_statistical_outliers(sl_ctx* c, const double* xyz, int64_t n, int nb_neig
   }
   py.levels = levels;
   py.l0 = l0;
+  // first-child tables of the levels above l0 (best-first search of isolated queries)
+  std::vector<DBuf<uint32_t>> lfc(kMaxLevels);
+  for (int l = l0 + 1; l < levels; ++l) {
+    MTRY(c, lfc[l].alloc(py.m[l] + 1));
+    hipLaunchKernelGGL(k_first_child, dim3(blocks(py.m[l] + 1)), dim3(kT), 0, s, lk[l].p, py.m[l], lk[l - 1].p,
+                       py.m[l - 1], lfc[l].p);
+    MTRY(c, hipGetLastError());
+    py.fchild[l] = lfc[l].p;
+  }
   MTRY(c, sxyz.alloc(3 * n));
   hipLaunchKernelGGL(k_gather_sorted, dim3(blocks(n)), dim3(kT), 0, s, xyz, idx.p, n, sxyz.p);
   MTRY(c, hipGetLastError());
@@ -976,12 +1157,36 @@ int sl_statistical_outliers(sl_ctx* c, const double* xyz, int64_t n, int nb_neig
   unsigned n_slow = 0;
   MTRY(c, hipMemcpyAsync(&n_slow, slow_n.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
   MTRY(c, hipStreamSynchronize(s));
+  DBuf<uint32_t> over_q;  // (function scope: freed after the final synchronisation)
+  DBuf<unsigned> over_n;
   if (n_slow) {
-    if (nb_neighbors == 20)
-      hipLaunchKernelGGL(k_knn_slow<20>, dim3(n_slow), dim3(64), 0, s, idx.p, n, py, nb_neighbors, avg_dist);
-    else
-      hipLaunchKernelGGL(k_knn_slow<kMaxK>, dim3(n_slow), dim3(64), 0, s, idx.p, n, py, nb_neighbors, avg_dist);
-    MTRY(c, hipGetLastError());
+    // best-first search; the rare frontier overflow climbs the pyramid (k_knn_slow)
+    const bool climb_only = getenv("SLGPU_MERGE_CLIMB") != nullptr;  // measurement only: the old path
+    unsigned n_over = n_slow;
+    if (!climb_only) {
+      MTRY(c, over_q.alloc(n_slow));
+      MTRY(c, over_n.alloc(1));
+      MTRY(c, hipMemsetAsync(over_n.p, 0, sizeof(unsigned), s));
+      if (nb_neighbors == 20)
+        hipLaunchKernelGGL(k_knn_best<20>, dim3(n_slow), dim3(64), 0, s, idx.p, n, py, nb_neighbors, avg_dist,
+                           over_q.p, over_n.p);
+      else
+        hipLaunchKernelGGL(k_knn_best<kMaxK>, dim3(n_slow), dim3(64), 0, s, idx.p, n, py, nb_neighbors, avg_dist,
+                           over_q.p, over_n.p);
+      MTRY(c, hipGetLastError());
+      MTRY(c, hipMemcpyAsync(&n_over, over_n.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+      MTRY(c, hipStreamSynchronize(s));
+    }
+    if (n_over) {
+      Pyramid pq = py;
+      if (!climb_only) pq.slow_q = over_q.p;
+      if (nb_neighbors == 20)
+        hipLaunchKernelGGL(k_knn_slow<20>, dim3(n_over), dim3(64), 0, s, idx.p, n, pq, nb_neighbors, avg_dist);
+      else
+        hipLaunchKernelGGL(k_knn_slow<kMaxK>, dim3(n_over), dim3(64), 0, s, idx.p, n, pq, nb_neighbors, avg_dist);
+      MTRY(c, hipGetLastError());
+    }
+    if (getenv("SLGPU_MERGE_STATS")) fprintf(stderr, "[slmerge] slow=%u overflow=%u\n", n_slow, climb_only ? 0u : n_over);
   }
   if (want_stats) {
     unsigned h[2 * kMaxLevels];

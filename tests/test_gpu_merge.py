@@ -135,3 +135,28 @@ def test_merge_posed_views_end_to_end(mg, tmp_path):
     np.testing.assert_array_equal(RC, VC[ind])
     with pytest.raises(ValueError):
         mg.merge_pro_360_posed(str(tmp_path / "none"), str(out), inv_poses)
+
+
+def test_isolated_points_best_first_equals_exhaustive(mg, monkeypatch):
+    """Isolated queries (far outliers, and a point at the centre of a dense
+    sphere shell, whose frontier overflows into the pyramid climb) through the
+    best-first search: the same means, bit for bit, as the exhaustive climb
+    (SLGPU_MERGE_CLIMB) and cKDTree's within rounding."""
+    from scipy.spatial import cKDTree
+    rng = np.random.default_rng(77)
+    n = 200_000
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    shell = u * 300.0
+    blob = rng.normal(size=(50_000, 3)) * 5.0 + np.array([900.0, 0.0, 0.0])
+    far = np.array([[0.0, 0.0, 0.0], [2000.0, 2000.0, 2000.0], [-1500.0, 30.0, 7.0], [905.0, 80.0, 0.0]])
+    P = np.concatenate([shell, blob, far])
+    ind, avg = mg.remove_statistical_outlier(P, 20, 2.0)
+    monkeypatch.setenv("SLGPU_MERGE_CLIMB", "1")
+    ind_c, avg_c = mg.remove_statistical_outlier(P, 20, 2.0)
+    monkeypatch.delenv("SLGPU_MERGE_CLIMB")
+    a = avg.cpu().numpy()
+    np.testing.assert_array_equal(a, avg_c.cpu().numpy())
+    np.testing.assert_array_equal(ind.cpu().numpy(), ind_c.cpu().numpy())
+    d, _ = cKDTree(P).query(P[-4:], k=20)
+    np.testing.assert_allclose(a[-4:], d.mean(1), rtol=1e-14)
