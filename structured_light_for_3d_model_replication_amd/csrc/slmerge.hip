@@ -109,14 +109,15 @@ __global__ __launch_bounds__(kT) void k_rs_count(const uint64_t* keys, int64_t n
   __shared__ uint32_t s_c[kRsBins];
   if (threadIdx.x < kRsBins) s_c[threadIdx.x] = 0u;
   __syncthreads();
-  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile + static_cast<int64_t>(threadIdx.x) * kRsItems;
+  // the tile's items in any order: lane-interleaved (coalesced) loads
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile + threadIdx.x;
   uint32_t c[kRsBins];
 #pragma unroll
   for (int d = 0; d < kRsBins; ++d) c[d] = 0u;
 #pragma unroll
   for (int j = 0; j < kRsItems; ++j) {
-    if (base + j < n) {
-      const unsigned d = digit_of(keys[base + j], shift);
+    if (base + j * kT < n) {
+      const unsigned d = digit_of(keys[base + j * kT], shift);
 #pragma unroll
       for (int e = 0; e < kRsBins; ++e) c[e] += (d == static_cast<unsigned>(e)) ? 1u : 0u;
     }
@@ -161,6 +162,9 @@ __global__ __launch_bounds__(kT) void k_rs_scatter(const uint64_t* kin, const ui
                                                    int tiles) {
   __shared__ uint32_t s[kRsBins * kT];  // [digit][thread] counts, then their exclusive scan
   __shared__ uint32_t s_part[kT];
+  __shared__ uint32_t s_start[kRsBins];  // tile-local start of every digit's run
+  __shared__ uint64_t s_k[kRsTile];      // the tile in stable digit order
+  __shared__ uint32_t s_v[kRsTile];
   const int t = threadIdx.x;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kRsTile + static_cast<int64_t>(t) * kRsItems;
   uint64_t k[kRsItems];
@@ -215,8 +219,11 @@ __global__ __launch_bounds__(kT) void k_rs_scatter(const uint64_t* kin, const ui
 #pragma unroll
   for (int j = 0; j < kRsBins; ++j) s[kRsBins * t + j] = pre + loc[j];
   __syncthreads();
-  // item j of thread t with digit d: global offset of (d, tile) + (d's items in
-  // earlier threads of the tile) + (d's items earlier in this thread)
+  // item j of thread t with digit d goes to its tile-local rank: (items with
+  // a smaller digit) + (d's items in earlier threads) + (d's items earlier in
+  // this thread) -- the stable order; the tile is reordered in LDS, then
+  // written out run by run (consecutive threads -> consecutive addresses)
+  if (t < kRsBins) s_start[t] = s[t * kT];
   uint32_t run[kRsBins];
 #pragma unroll
   for (int d = 0; d < kRsBins; ++d) run[d] = 0u;
@@ -231,11 +238,20 @@ __global__ __launch_bounds__(kT) void k_rs_scatter(const uint64_t* kin, const ui
           r = run[e];
           ++run[e];
         }
-      const uint32_t pos =
-          offs[static_cast<int64_t>(d) * tiles + blockIdx.x] + (s[d * kT + t] - s[d * kT]) + r;
-      kout[pos] = k[j];
-      vout[pos] = v[j];
+      const uint32_t rank = s[d * kT + t] + r;
+      s_k[rank] = k[j];
+      s_v[rank] = v[j];
     }
+  }
+  __syncthreads();
+  const int64_t tile0 = static_cast<int64_t>(blockIdx.x) * kRsTile;
+  const int tn = static_cast<int>(min<int64_t>(kRsTile, n - tile0));
+  for (int i = t; i < tn; i += kT) {
+    const uint64_t key = s_k[i];
+    const unsigned d = digit_of(key, shift);
+    const uint32_t pos = offs[static_cast<int64_t>(d) * tiles + blockIdx.x] + (static_cast<uint32_t>(i) - s_start[d]);
+    kout[pos] = key;
+    vout[pos] = s_v[i];
   }
 }
 
@@ -898,13 +914,21 @@ int radix_sort(sl_ctx* c, uint64_t* keys, uint32_t* vals, int64_t n, int bits, h
   MTRY(c, k2.alloc(n));
   MTRY(c, v2.alloc(n));
   MTRY(c, cnt.alloc(static_cast<int64_t>(kRsBins) * tiles));
+  // exclusive scan of the digit-major counts: tile sums, one workgroup over
+  // them, local scans (in place)
+  const int64_t n_cnt = static_cast<int64_t>(kRsBins) * tiles;
+  const int ctiles = static_cast<int>((n_cnt + kRsTile - 1) / kRsTile);
+  DBuf<uint32_t> csum;
+  MTRY(c, csum.alloc(ctiles));
   uint64_t *ka = keys, *kb = k2.p;
   uint32_t *va = vals, *vb = v2.p;
   int passes = 0;
   for (int shift = 0; shift < bits; shift += kRsBits, ++passes) {
     hipLaunchKernelGGL(k_rs_count, dim3(tiles), dim3(kT), 0, s, ka, n, shift, cnt.p, tiles);
-    hipLaunchKernelGGL(k_scan1, dim3(1), dim3(kT), 0, s, cnt.p, static_cast<int64_t>(kRsBins) * tiles,
+    hipLaunchKernelGGL(k_tile_sums, dim3(ctiles), dim3(kT), 0, s, cnt.p, n_cnt, csum.p);
+    hipLaunchKernelGGL(k_scan1, dim3(1), dim3(kT), 0, s, csum.p, static_cast<int64_t>(ctiles),
                        static_cast<uint32_t*>(nullptr));
+    hipLaunchKernelGGL(k_tile_scan, dim3(ctiles), dim3(kT), 0, s, cnt.p, n_cnt, csum.p, cnt.p);
     hipLaunchKernelGGL(k_rs_scatter, dim3(tiles), dim3(kT), 0, s, ka, va, kb, vb, n, shift, cnt.p, tiles);
     MTRY(c, hipGetLastError());
     std::swap(ka, kb);
