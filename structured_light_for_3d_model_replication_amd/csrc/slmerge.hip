@@ -875,6 +875,13 @@ __global__ __launch_bounds__(kT) void k_transform(double* xyz, int64_t n, const 
 // ------------------------------------------------------------------ host ----
 unsigned blocks(int64_t n) { return static_cast<unsigned>((n + kT - 1) / kT); }
 
+struct PinBuf {
+  double* p = nullptr;
+  ~PinBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
 template <typename T>
 struct DBuf {
   T* p = nullptr;
@@ -1222,20 +1229,61 @@ int sl_statistical_outliers(sl_ctx* c, const double* xyz, int64_t n, int nb_neig
     fprintf(stderr, "\n");
   }
   // cloud mean / std of the positive means: sequential, as std::accumulate /
-  // std::inner_product in RemoveStatisticalOutliers
-  std::vector<double> a(static_cast<size_t>(n));
-  MTRY(c, hipMemcpyAsync(a.data(), avg_dist, sizeof(double) * a.size(), hipMemcpyDeviceToHost, s));
-  MTRY(c, hipStreamSynchronize(s));
+  // std::inner_product in RemoveStatisticalOutliers.  The means stream to the
+  // host through two pinned 1 MB buffers, the copy of one chunk overlapping
+  // the (latency-bound) accumulation of the other; the conditional terms are
+  // selects, m + (v > 0 ? v : +0.0) -- bit-identical to skipping, m >= +0.
   int64_t valid = 0;
-  double mean = 0.0;
-  for (double v : a) {
-    if (v > 0) mean = mean + v;
+  double mean = 0.0, sq = 0.0;
+  {
+    constexpr int64_t kCh = int64_t{1} << 17;  // doubles per chunk
+    PinBuf pin;
+    MTRY(c, hipHostMalloc(reinterpret_cast<void**>(&pin.p), sizeof(double) * 2 * kCh, hipHostMallocDefault));
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    struct EvGuard {
+      hipEvent_t* e;
+      ~EvGuard() {
+        for (int i = 0; i < 2; ++i)
+          if (e[i]) (void)hipEventDestroy(e[i]);
+      }
+    } evg{ev};
+    for (int i = 0; i < 2; ++i) MTRY(c, hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    const int64_t nch = (n + kCh - 1) / kCh;
+    auto enqueue = [&](int64_t ch) -> hipError_t {
+      const int64_t lo = ch * kCh, cnt = std::min(kCh, n - lo);
+      hipError_t e = hipMemcpyAsync(pin.p + (ch & 1) * kCh, avg_dist + lo, sizeof(double) * cnt,
+                                    hipMemcpyDeviceToHost, s);
+      return e == hipSuccess ? hipEventRecord(ev[ch & 1], s) : e;
+    };
+    for (int pass = 0; pass < 2; ++pass) {
+      MTRY(c, enqueue(0));
+      if (nch > 1) MTRY(c, enqueue(1));
+      for (int64_t ch = 0; ch < nch; ++ch) {
+        MTRY(c, hipEventSynchronize(ev[ch & 1]));
+        const double* v = pin.p + (ch & 1) * kCh;
+        const int64_t cnt = std::min(kCh, n - ch * kCh);
+        if (pass == 0) {
+          double m = mean;
+          int64_t va = valid;
+          for (int64_t i = 0; i < cnt; ++i) {
+            m = m + (v[i] > 0 ? v[i] : 0.0);
+            va += v[i] >= 0.0 ? 1 : 0;  // every point has >= 1 neighbour (itself)
+          }
+          mean = m;
+          valid = va;
+        } else {
+          double q = sq;
+          for (int64_t i = 0; i < cnt; ++i) q = q + (v[i] > 0 ? (v[i] - mean) * (v[i] - mean) : 0);
+          sq = q;
+        }
+        if (ch + 2 < nch) MTRY(c, enqueue(ch + 2));
+      }
+      if (pass == 0) {
+        if (valid == 0) return SL_OK;
+        mean /= static_cast<double>(valid);
+      }
+    }
   }
-  for (double v : a) valid += (v >= 0.0) ? 1 : 0;  // every point has >= 1 neighbour (itself)
-  if (valid == 0) return SL_OK;
-  mean /= static_cast<double>(valid);
-  double sq = 0.0;
-  for (double v : a) sq = sq + (v > 0 ? (v - mean) * (v - mean) : 0);
   const double sd = sqrt(sq / static_cast<double>(valid - 1));
   const double thr = mean + std_ratio * sd;
   hipLaunchKernelGGL(k_keep_flags, dim3(blocks(n)), dim3(kT), 0, s, avg_dist, n, thr, flag.p);
