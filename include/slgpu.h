@@ -149,6 +149,15 @@ int sl_profile_enable(sl_ctx* ctx, int max_calls);
  * recorded calls since the last read, and their count; restarts recording. */
 int sl_profile_read(sl_ctx* ctx, double* decode_ms, double* count_ms, double* cloud_ms, int* calls);
 
+/* Blocking, measurement only: re-launches the kernels of the last launch group
+ * of the previous sl_decode_triangulate / sl_triangulate_maps call `reps`
+ * times each, back to back on its stream, and returns each kernel's average
+ * duration from HIP events around the `reps` launches (the events' own cost
+ * amortised).  k_count and k_cloud run first: the call's outputs are rewritten
+ * with the same values; the adaptive-threshold histograms k_decode's re-runs
+ * accumulate into are reset for later calls. */
+int sl_time_kernels(sl_ctx* ctx, int reps, double* decode_ms, double* count_ms, double* cloud_ms);
+
 /* ASCII PLY of a cloud exactly as the reference writes it (sl_system.py:665-691,
  * multi_point_cloud_process.py:121-131): header, then per point
  * "%.4f %.4f %.4f %d %d %d\n" of x, y, z and the colour swapped from BGR to

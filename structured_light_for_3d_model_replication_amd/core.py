@@ -283,6 +283,16 @@ class Reconstructor:
                                                ctypes.byref(n)), self._ctx, "sl_profile_read")
         return a.value, b.value, c.value, n.value
 
+    def time_kernels(self, reps: int = 20):
+        """Measurement only: each kernel of the last call's last launch group
+        re-run ``reps`` times back to back -> (k_decode ms, k_count ms,
+        k_cloud ms) averages from HIP events around the repeats."""
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        with self._lock:
+            _lib.check(self._L.sl_time_kernels(self._ctx, int(reps), ctypes.byref(a), ctypes.byref(b),
+                                               ctypes.byref(c)), self._ctx, "sl_time_kernels")
+        return a.value, b.value, c.value
+
     def last_thresholds(self, view: int = 0):
         nf, dr = ctypes.c_float(), ctypes.c_float()
         tw, tc = ctypes.c_int(), ctypes.c_int()

@@ -1279,6 +1279,14 @@ struct sl_ctx {
   std::vector<hipEvent_t> prof_ev;  // kProfEv events per call slot
   std::vector<int> prof_groups;     // launch groups recorded per call
   int prof_n = 0;
+  // the last launch group's kernels and arguments (sl_time_kernels)
+  struct {
+    bool valid = false;
+    Params p[3];
+    const void* fn[3] = {nullptr, nullptr, nullptr};  // k_decode, k_count, k_cloud (or null)
+    dim3 grid;
+    hipStream_t s = nullptr;
+  } last;
 };
 
 namespace {
@@ -1412,10 +1420,16 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->par = b;
     }
     const dim3 grid(static_cast<unsigned>((cpv + kWaves - 1) / kWaves), static_cast<unsigned>(nv));
+    c->last.valid = true;
+    c->last.grid = grid;
+    c->last.s = s;
+    c->last.fn[2] = nullptr;
     {
       p.mode = decode_mode;
       void* args[] = {&p};
       KernelFn fn = pick_decode(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode, vec);
+      c->last.p[0] = p;
+      c->last.fn[0] = reinterpret_cast<const void*>(fn);
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(kThreads), args, 0, s));
     }
     if (gev) HIP_TRY(c, hipEventRecord(gev[1], s));
@@ -1423,6 +1437,8 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       p.mode = count_mode;
       void* args[] = {&p};
       const void* fn = vec ? reinterpret_cast<const void*>(k_count<1>) : reinterpret_cast<const void*>(k_count<0>);
+      c->last.p[1] = p;
+      c->last.fn[1] = fn;
       HIP_TRY(c, hipLaunchKernel(fn, grid, dim3(kThreads), args, 0, s));
     }
     if (gev) HIP_TRY(c, hipEventRecord(gev[2], s));
@@ -1430,6 +1446,8 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       p.mode = cloud_mode;
       void* args[] = {&p};
       KernelFn fn = pick_cloud(cloud_mode, vec);
+      c->last.p[2] = p;
+      c->last.fn[2] = reinterpret_cast<const void*>(fn);
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(kThreads), args, 0, s));
     }
     if (gev) HIP_TRY(c, hipEventRecord(gev[3], s));
@@ -1863,6 +1881,52 @@ int sl_profile_read(sl_ctx* c, double* decode_ms, double* count_ms, double* clou
   if (calls) *calls = c->prof_n;
   c->prof_n = 0;
   return SL_OK;
+}
+
+int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, double* cloud_ms) {
+  if (!c || reps < 1) return SL_EINVAL;
+  if (!c->last.valid) return fail(c, SL_EINVAL, "sl_time_kernels: no earlier call to re-run");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->last.s;
+  hipEvent_t ev[4];
+  for (int k = 0; k < 4; ++k) HIP_TRY(c, hipEventCreate(&ev[k]));
+  int r = SL_OK;
+  // k_count and k_cloud first: they read k_decode's records and histogram,
+  // which k_decode's re-runs then overwrite (records identically; the
+  // histograms accumulate and are reset below)
+  const int order[3] = {1, 2, 0};
+  HIP_TRY(c, hipEventRecord(ev[0], s));
+  for (int q = 0; q < 3 && r == SL_OK; ++q) {
+    const int k = order[q];
+    if (c->last.fn[k]) {
+      Params p = c->last.p[k];
+      void* args[] = {&p};
+      for (int i = 0; i < reps; ++i) {
+        const hipError_t e = hipLaunchKernel(c->last.fn[k], c->last.grid, dim3(kThreads), args, 0, s);
+        if (e != hipSuccess) {
+          r = fail(c, SL_EHIP, std::string("sl_time_kernels: ") + hipGetErrorString(e));
+          break;
+        }
+      }
+    }
+    if (hipEventRecord(ev[q + 1], s) != hipSuccess && r == SL_OK) r = fail(c, SL_EHIP, "hipEventRecord");
+  }
+  double out[3] = {0.0, 0.0, 0.0};
+  if (r == SL_OK && hipEventSynchronize(ev[3]) == hipSuccess) {
+    for (int q = 0; q < 3; ++q) {
+      float ms = 0.f;
+      const int k = order[q];
+      if (hipEventElapsedTime(&ms, ev[q], ev[q + 1]) == hipSuccess) out[k] = c->last.fn[k] ? ms / reps : 0.0;
+    }
+  }
+  for (int k = 0; k < 4; ++k) (void)hipEventDestroy(ev[k]);
+  // the re-runs accumulated into the histograms: the next calls start from zero
+  for (int b = 0; b < 2; ++b) c->hist_dirty[b] = c->cap_hist[b] / kSlot;
+  c->last.valid = false;
+  if (decode_ms) *decode_ms = out[0];
+  if (count_ms) *count_ms = out[1];
+  if (cloud_ms) *cloud_ms = out[2];
+  return r;
 }
 
 int sl_last_thresholds(sl_ctx* c, int view, float* nf, float* dr, int* thr_w, int* thr_c) {

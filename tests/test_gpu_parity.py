@@ -325,3 +325,25 @@ def test_multigroup_call_on_a_caller_stream(eng):
     s.synchronize()
     assert int(n.item()) == ref_off[-1]
     assert float(tot.item()) == ref_sum
+
+
+def test_time_kernels_keeps_outputs_and_later_calls_exact(eng):
+    """sl_time_kernels (measurement) re-runs the last call's kernels: positive
+    durations, the call's outputs unchanged, and the next call (histograms
+    reset) still bit-exact."""
+    rig, st, tex, cal = _render(480, 640, 1920, 1080, seed=21)
+    sth, texh = st.cpu().numpy(), tex.cpu().numpy()
+    col, row, mask, P, C = o.decode_triangulate(list(sth), texh, cal)
+    for _ in range(2):
+        res = _run(eng, sth, texh, cal, 1920, 1080, xyz_dtype=torch.float32)
+        t = eng.time_kernels(3)
+        assert all(x > 0 for x in t)
+        eng.sync()
+        np.testing.assert_array_equal(res["col_map"][0].cpu().numpy(), col)
+        np.testing.assert_array_equal(res["mask"][0].cpu().numpy(), mask)
+        xyz, bgr, off = _cloud_np(res["cloud"])
+        assert off[-1] == len(P)
+        _assert_f32(xyz, P)
+        np.testing.assert_array_equal(bgr, C)
+    with pytest.raises(ValueError):
+        eng.time_kernels(3)  # nothing left to re-run
