@@ -72,11 +72,25 @@ def process_batch(parent_dir, calib_data, *, n_cols=1920, n_rows=1080, device=No
     and only the planes the cloud reads are decoded and uploaded.  Otherwise
     all stacks are read first and decoded + triangulated in ONE fused GPU
     launch (merged cloud, per-view offsets)."""
+    return process_views(view_folders(parent_dir, log), calib_data, n_cols=n_cols, n_rows=n_rows, device=device,
+                         write=write, log=log, streamed=streamed, slots=slots, keep=keep)
+
+
+def view_folders(parent_dir, log=print) -> list:
+    """The batch loop's views (multi_point_cloud_process.py:241-247): sorted
+    subfolders that hold images; the others are reported and skipped."""
     subfolders = sorted(f.path for f in os.scandir(parent_dir) if f.is_dir())
     views = [f for f in subfolders if io.list_stack_files(f)]
     for f in subfolders:
         if f not in views:
             log(f"Skipping {os.path.basename(f)} (No images found).")
+    return views
+
+
+def process_views(views, calib_data, *, n_cols=1920, n_rows=1080, device=None, write=True, log=print,
+                  streamed=True, slots=3, keep=True):
+    """process_batch on a given list of view folders (the shard of one rank in
+    a multi-GPU scan, scan360.py).  Returns {folder: (P, C)}."""
     if not views:
         return {}
     if streamed:
