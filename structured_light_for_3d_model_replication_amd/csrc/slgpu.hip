@@ -877,9 +877,15 @@ constexpr int kPipe = SLGPU_PIPE;  // points per lane per pass in k_cloud
 #endif
 constexpr bool kStageOut = SLGPU_STAGE_OUT != 0;  // f32 points leave through an LDS stage
 #ifndef SLGPU_LDS_BGR
-#define SLGPU_LDS_BGR 1
+#define SLGPU_LDS_BGR 2
 #endif
-constexpr bool kLdsBgr = SLGPU_LDS_BGR != 0;  // compacted colours in LDS (else re-read from the texture)
+// colour of a point: 1 = compacted with the entries in LDS, 2 = the chunk's
+// texture bytes in LDS in pixel order (3 B/px; 12 KB less LDS per workgroup
+// than 1), 0 = re-read from the texture in global memory
+constexpr int kBgrMode = SLGPU_LDS_BGR;
+constexpr bool kLdsBgr = kBgrMode == 1;
+constexpr bool kTexLds = kBgrMode == 2;
+constexpr int kBgrWords = kLdsBgr ? kChunk : kTexLds ? 3 * kChunk / 4 + 4 : 4;  // u32 per wave
 
 template <int MODE>
 __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
@@ -950,7 +956,17 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
     return;
   }
 
-  // ---- 2. compacted entries in LDS ----
+  // ---- 2. compacted entries in LDS (and the chunk's colours, kTexLds) ----
+  if (kTexLds) {
+    uint4* t4 = reinterpret_cast<uint4*>(s_bgr);
+    if (has_tex) {
+      t4[3 * lane] = tq[0];
+      t4[3 * lane + 1] = tq[1];
+      t4[3 * lane + 2] = tq[2];
+    } else {
+      t4[lane] = tq[0];  // gray bytes, one per pixel
+    }
+  }
   {
     int idx = incl - n_l;
 #pragma unroll
@@ -967,6 +983,7 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
       if ((ptbits >> k) & 1u) {
         s_ent[idx] = static_cast<uint32_t>(lane * kPx + k) | (code << 10);
         if (kLdsBgr) s_bgr[idx] = bgr;
+        (void)bgr;
       }
       idx += (ptbits >> k) & 1u;
     }
@@ -998,6 +1015,14 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
   const int dbg = p.dbg;
   auto point_bgr = [&](int j, int local) -> uint32_t {
     if (kLdsBgr) return s_bgr[j];
+    if (kTexLds) {
+      if (has_tex) {  // bytes 3 local .. 3 local + 2 of the chunk's BGR
+        const int b = 3 * local;
+        const uint32_t w0 = s_bgr[b >> 2], w1 = s_bgr[(b >> 2) + 1];
+        return __builtin_amdgcn_alignbyte(w1, w0, static_cast<unsigned>(b & 3)) & 0xffffffu;
+      }
+      return ((s_bgr[local >> 2] >> (8 * (local & 3))) & 0xffu) * 0x010101u;
+    }
     if (has_tex) {
       const uint8_t* t = p.tex + view * p.tex_vs + 3 * (cpx + local);
       return t[0] | (static_cast<uint32_t>(t[1]) << 8) | (static_cast<uint32_t>(t[2]) << 16);
@@ -1206,7 +1231,7 @@ constexpr int kPrefixBatch = 4;
 template <int MODE, int VEC>
 __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
   __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
-  __shared__ uint32_t s_bgr[kWaves][kLdsBgr ? kChunk : 1];  // their B | G << 8 | R << 16
+  __shared__ __attribute__((aligned(16))) uint32_t s_bgr[kWaves][kBgrWords];  // colours (kBgrMode)
   __shared__ float s_sxyz[kWaves][kStageOut ? 192 : 1];      // output stage: 64 points' xyz
   __shared__ uint8_t s_scol[kWaves][kStageOut ? 192 : 4];    // and their colour bytes
   __shared__ long long s_wred[kWaves];
