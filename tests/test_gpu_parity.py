@@ -376,3 +376,21 @@ def test_full_12mp_posed_views_cloud_only_vs_oracle(eng):
         assert off[v + 1] - off[v] == len(P)
         np.testing.assert_array_equal(xyz[off[v]:off[v + 1]].view(np.uint64), P.view(np.uint64))
         np.testing.assert_array_equal(bgr[off[v]:off[v + 1]], C)
+
+
+@pytest.mark.parametrize("H,W", [(1, 1), (1, 17), (3, 1), (2, 1023), (1, 1025), (5, 64)])
+def test_tiny_and_ragged_frames_vs_oracle(eng, H, W):
+    """Degenerate frame shapes: single pixel, single row / column, a chunk
+    boundary straddled by one pixel (1023, 1025 px); maps and cloud bit-exact
+    vs the oracle (adaptive thresholds over so few pixels included)."""
+    rig, st, tex, cal = _render(H, W, 1920, 1080, seed=H * 1000 + W, device="cpu")
+    sth, texh = st.numpy(), tex.numpy()
+    col, row, mask, P, C = o.decode_triangulate(list(sth), texh, cal)
+    res = _run(eng, sth, texh, cal, 1920, 1080, xyz_dtype=torch.float64)
+    np.testing.assert_array_equal(res["col_map"][0].cpu().numpy(), col)
+    np.testing.assert_array_equal(res["row_map"][0].cpu().numpy(), row)
+    np.testing.assert_array_equal(res["mask"][0].cpu().numpy(), mask)
+    xyz, bgr, off = _cloud_np(res["cloud"])
+    assert off[-1] == len(P)
+    np.testing.assert_array_equal(xyz.view(np.uint64), P.view(np.uint64))
+    np.testing.assert_array_equal(bgr, C)
