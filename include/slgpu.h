@@ -207,6 +207,36 @@ int sl_select_by_index(sl_ctx* ctx, const double* xyz, const uint8_t* bgr, const
  * ((m0 x + m1 y) + m2 z) + m3 -- PointCloud::Transform.  Asynchronous. */
 int sl_transform_points(sl_ctx* ctx, double* xyz, int64_t n, const double* pose, void* stream);
 
+/* ---- multi-GPU gather ----
+ * The merge's one exchange: every rank's cloud to `root` in rank order over
+ * RCCL (opened with dlopen by soname, so a process that already holds
+ * PyTorch's RCCL shares that copy).  One context per rank (GPU):
+ *   sl_gather_unique_id  one rank makes the 128-byte id, shared out of band
+ *                        (the Python side uses torch.distributed.broadcast_object_list);
+ *   sl_gather_init       ncclCommInitRank on the context's device;
+ *   sl_gather_counts     blocking: an ncclAllGather of one int64 per rank ->
+ *                        counts_out[nranks] (host) on every rank, so the root
+ *                        can size its buffers;
+ *   sl_gather            grouped ncclSend / ncclRecv of xyz (f32 or f64, 3 per
+ *                        point) and bgr (3 B per point) into the root's
+ *                        xyz_out / bgr_out at exclusive-scan offsets of
+ *                        `counts`; asynchronous on `stream`.
+ * Replaces the sequential per-file merge of processing.py:116-140. */
+int sl_gather_unique_id(uint8_t* id_out /* 128 bytes */);
+int sl_gather_init(sl_ctx* ctx, int nranks, int rank, const uint8_t* id /* 128 bytes */);
+int sl_gather_counts(sl_ctx* ctx, int64_t n_local, int64_t* counts_out, void* stream);
+int sl_gather(sl_ctx* ctx, const void* xyz, int xyz_dtype, const uint8_t* bgr, const int64_t* counts, int root,
+              void* xyz_out, uint8_t* bgr_out, void* stream);
+
+/* The names of SURVEY.md §8(b): sl_decode_triangulate is already batched (V
+ * views per call); sl_last_error is sl_ctx_last_error. */
+int sl_decode_triangulate_batch(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_stride, int n_views,
+                                int n_img, int H, int W, int n_cols, int n_rows, const uint8_t* tex_bgr,
+                                int64_t tex_view_stride, int mask_mode, const double* poses, int32_t* col_out,
+                                int32_t* row_out, uint8_t* mask_out, void* xyz_out, int xyz_dtype,
+                                uint8_t* bgr_out, int64_t out_capacity, int64_t* view_offsets, void* stream);
+const char* sl_last_error(const sl_ctx* ctx);
+
 /* ---- calibration products (csrc/slcalib.hip) ----
  * Replaces the NumPy tail of SLSystem.calibrate_final (server/sl_system.py:348-403):
  * from the stereo parameters OpenCV estimated (cam_K = K1, proj_K = K2, R, T;

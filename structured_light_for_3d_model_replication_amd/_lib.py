@@ -34,7 +34,9 @@ EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_err
            "sl_set_calib", "sl_decode_triangulate", "sl_triangulate_maps", "sl_sync",
            "sl_last_thresholds", "sl_profile_enable", "sl_profile_read", "sl_time_kernels", "sl_format_ply", "sl_write_ply",
            "sl_write_ply_binary", "sl_voxel_downsample", "sl_statistical_outliers", "sl_select_by_index",
-           "sl_transform_points", "sl_calib_products")
+           "sl_transform_points", "sl_calib_products", "sl_gather_unique_id", "sl_gather_init", "sl_gather_counts",
+           "sl_gather",
+           "sl_decode_triangulate_batch", "sl_last_error")
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -65,6 +67,13 @@ _SIGS = {
     "sl_statistical_outliers": (_i32, [_vp, _vp, _i64, _i32, ctypes.c_double, _vp, _vp, ctypes.POINTER(_i64), _vp]),
     "sl_select_by_index": (_i32, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "sl_transform_points": (_i32, [_vp, _vp, _i64, _vp, _vp]),
+    "sl_gather_unique_id": (_i32, [_vp]),
+    "sl_gather_init": (_i32, [_vp, _i32, _i32, _vp]),
+    "sl_gather_counts": (_i32, [_vp, _i64, _vp, _vp]),
+    "sl_gather": (_i32, [_vp, _vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp]),
+    "sl_decode_triangulate_batch": (_i32, [_vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32,
+                                           _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp]),
+    "sl_last_error": (ctypes.c_char_p, [_vp]),
     "sl_calib_products": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp]),
 }
 

@@ -265,6 +265,53 @@ class Reconstructor:
                                                  self._stream(stream)), self._ctx, "sl_calib_products")
         return nc, col, row
 
+    # ------------------------------------------------------------ gather
+    @staticmethod
+    def gather_unique_id() -> bytes:
+        """A new RCCL unique id (128 bytes) for ``gather_init`` on every rank."""
+        L = _lib.load()
+        buf = ctypes.create_string_buffer(128)
+        _lib.check(L.sl_gather_unique_id(buf), None, "sl_gather_unique_id (is librccl.so available?)")
+        return buf.raw
+
+    def gather_init(self, nranks: int, rank: int, unique_id: bytes) -> None:
+        """RCCL communicator of this context (one per rank / GPU)."""
+        if len(unique_id) != 128:
+            raise ValueError("unique_id must be 128 bytes")
+        with self._lock:
+            _lib.check(self._L.sl_gather_init(self._ctx, int(nranks), int(rank), unique_id), self._ctx,
+                       "sl_gather_init")
+            self._gather = (int(nranks), int(rank))
+
+    def gather(self, xyz: torch.Tensor, bgr: torch.Tensor, root: int = 0, stream=None):
+        """Every rank's (xyz [n,3] f32/f64, bgr [n,3] u8) to ``root`` in rank
+        order over RCCL (sl_gather_counts + sl_gather).  -> (xyz_all,
+        bgr_all, counts) on the root, (None, None, counts) elsewhere."""
+        nranks, rank = getattr(self, "_gather", (0, 0))
+        if not nranks:
+            raise ValueError("gather_init has not been called")
+        if xyz.dtype not in (torch.float32, torch.float64) or bgr.dtype != torch.uint8:
+            raise ValueError("xyz must be float32/float64 and bgr uint8")
+        xyz = xyz.to(self.device).contiguous()
+        bgr = bgr.to(self.device).contiguous()
+        n = xyz.shape[0]
+        if xyz.shape != (n, 3) or bgr.shape != (n, 3):
+            raise ValueError("xyz and bgr must be [n, 3]")
+        counts = (ctypes.c_int64 * nranks)()
+        xdt = _lib.SL_XYZ_F64 if xyz.dtype == torch.float64 else _lib.SL_XYZ_F32
+        st = self._stream(stream)
+        with self._lock:
+            _lib.check(self._L.sl_gather_counts(self._ctx, n, counts, st), self._ctx, "sl_gather_counts")
+            total = int(sum(counts))
+            xo = bo = None
+            if rank == root:
+                xo = torch.empty((total, 3), dtype=xyz.dtype, device=self.device)
+                bo = torch.empty((total, 3), dtype=torch.uint8, device=self.device)
+            _lib.check(self._L.sl_gather(self._ctx, _ptr(xyz) if n else None, xdt, _ptr(bgr) if n else None,
+                                         counts, int(root), _ptr(xo) if total else None,
+                                         _ptr(bo) if total else None, st), self._ctx, "sl_gather")
+        return xo, bo, list(counts)
+
     def sync(self, stream=None) -> None:
         """Wait for this context's work and raise on device-side failures."""
         with self._lock:

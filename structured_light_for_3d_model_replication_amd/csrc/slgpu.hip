@@ -44,6 +44,11 @@
 #include <thread>
 #include <vector>
 
+#include <dlfcn.h>
+
+#include <mutex>
+
+#include "rccl/rccl.h"
 #include "slgpu.h"
 
 #pragma clang fp contract(off)
@@ -1305,6 +1310,11 @@ struct sl_ctx {
   std::vector<int> prof_groups;     // launch groups recorded per call
   int prof_n = 0;
   // the last launch group's kernels and arguments (sl_time_kernels)
+  // RCCL gather (sl_gather_init): communicator, this rank, count scratch
+  void* comm = nullptr;
+  int nranks = 0, rank = 0;
+  int64_t* d_gcounts = nullptr;
+  int64_t cap_gcounts = 0;
   struct {
     bool valid = false;
     Params p[3];
@@ -1313,6 +1323,63 @@ struct sl_ctx {
     hipStream_t s = nullptr;
   } last;
 };
+
+// ---------------------------------------------------------------- gather ----
+// The merge's one exchange: every rank's cloud to the root
+// rank in rank order, over RCCL (xGMI within a node).  RCCL is opened with
+// dlopen by soname, so a process that already holds one (PyTorch's) shares
+// that copy.  Counts: an ncclAllGather of one int64 per rank; payloads:
+// grouped ncclSend (every rank) / ncclRecv (root) straight into the root's
+// merged buffers at exclusive-scan offsets (RCCL has no gatherv, and a ring
+// all-gather would push every payload over every link).
+namespace {
+
+struct Rccl {
+  void* lib = nullptr;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+Rccl* rccl() {  // loaded once per process; null if RCCL is missing
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+      r.lib = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (r.lib) break;
+    }
+    if (!r.lib) return;
+    auto sym = [](const char* n) { return dlsym(r.lib, n); };
+    r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(sym("ncclGetUniqueId"));
+    r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(sym("ncclCommInitRank"));
+    r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(sym("ncclCommDestroy"));
+    r.all_gather = reinterpret_cast<decltype(r.all_gather)>(sym("ncclAllGather"));
+    r.send = reinterpret_cast<decltype(r.send)>(sym("ncclSend"));
+    r.recv = reinterpret_cast<decltype(r.recv)>(sym("ncclRecv"));
+    r.group_start = reinterpret_cast<decltype(r.group_start)>(sym("ncclGroupStart"));
+    r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
+    r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_gather || !r.send || !r.recv ||
+        !r.group_start || !r.group_end || !r.error_string)
+      r.lib = nullptr;
+  });
+  return r.lib ? &r : nullptr;
+}
+
+#define NCCL_TRY(ctx, expr)                                                                  \
+  do {                                                                                       \
+    ncclResult_t e_ = (expr);                                                                \
+    if (e_ != ncclSuccess) return fail((ctx), SL_EHIP, std::string(#expr) + ": " + R->error_string(e_)); \
+  } while (0)
+
+}  // namespace
 
 namespace {
 
@@ -1621,6 +1688,10 @@ int sl_ctx_create(int device, sl_ctx** out) {
 void sl_ctx_destroy(sl_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  if (c->comm) {
+    if (Rccl* R = rccl()) (void)R->comm_destroy(static_cast<ncclComm_t>(c->comm));
+  }
+  if (c->d_gcounts) (void)hipFree(c->d_gcounts);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (void* ptr : {static_cast<void*>(c->d_planes), static_cast<void*>(c->d_xn), static_cast<void*>(c->d_yn),
                     static_cast<void*>(c->d_nc), static_cast<void*>(c->d_stats), static_cast<void*>(c->d_f32),
@@ -2045,6 +2116,111 @@ int sl_write_ply_binary(const char* path, const void* xyz, int xyz_dtype, const 
   if (ok && n) ok = fwrite(body.data(), 1, body.size(), f) == body.size();
   ok = (fclose(f) == 0) && ok;
   return ok ? SL_OK : SL_EIO;
+}
+
+}  // extern "C"
+
+
+extern "C" {
+
+int sl_gather_unique_id(uint8_t* id_out) {
+  Rccl* R = rccl();
+  if (!id_out) return SL_EINVAL;
+  if (!R) return SL_EHIP;
+  ncclUniqueId id;
+  if (R->get_unique_id(&id) != ncclSuccess) return SL_EHIP;
+  memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+  return SL_OK;
+}
+
+int sl_gather_init(sl_ctx* c, int nranks, int rank, const uint8_t* id) {
+  if (!c) return SL_EINVAL;
+  if (nranks < 1 || rank < 0 || rank >= nranks || !id) return fail(c, SL_EINVAL, "sl_gather_init: bad rank / id");
+  Rccl* R = rccl();
+  if (!R) return fail(c, SL_EHIP, "sl_gather_init: RCCL (librccl.so) could not be loaded");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->comm) {
+    (void)R->comm_destroy(static_cast<ncclComm_t>(c->comm));
+    c->comm = nullptr;
+  }
+  ncclUniqueId uid;
+  memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t comm = nullptr;
+  NCCL_TRY(c, R->comm_init_rank(&comm, nranks, uid, rank));
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  return grow(c, &c->d_gcounts, &c->cap_gcounts, 2 * static_cast<int64_t>(nranks));
+}
+
+int sl_gather_counts(sl_ctx* c, int64_t n_local, int64_t* counts_out, void* stream) {
+  if (!c) return SL_EINVAL;
+  if (!c->comm) return fail(c, SL_EINVAL, "sl_gather_counts: sl_gather_init has not been called");
+  if (n_local < 0 || !counts_out) return fail(c, SL_EINVAL, "sl_gather_counts: bad arguments");
+  Rccl* R = rccl();
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIP_TRY(c, hipSetDevice(c->device));
+  int64_t* d_mine = c->d_gcounts + c->nranks;
+  HIP_TRY(c, hipMemcpyAsync(d_mine, &n_local, sizeof(int64_t), hipMemcpyHostToDevice, s));
+  NCCL_TRY(c, R->all_gather(d_mine, c->d_gcounts, 1, ncclInt64, static_cast<ncclComm_t>(c->comm), s));
+  HIP_TRY(c, hipMemcpyAsync(counts_out, c->d_gcounts, sizeof(int64_t) * c->nranks, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return SL_OK;
+}
+
+int sl_gather(sl_ctx* c, const void* xyz, int xyz_dtype, const uint8_t* bgr, const int64_t* counts, int root,
+              void* xyz_out, uint8_t* bgr_out, void* stream) {
+  if (!c) return SL_EINVAL;
+  if (!c->comm) return fail(c, SL_EINVAL, "sl_gather: sl_gather_init has not been called");
+  if (root < 0 || root >= c->nranks || !counts) return fail(c, SL_EINVAL, "sl_gather: bad arguments");
+  if (xyz_dtype != SL_XYZ_F32 && xyz_dtype != SL_XYZ_F64) return fail(c, SL_EINVAL, "sl_gather: bad xyz_dtype");
+  const int64_t n_local = counts[c->rank];
+  if (n_local < 0 || (n_local && (!xyz || !bgr))) return fail(c, SL_EINVAL, "sl_gather: bad local cloud");
+  int64_t total = 0;
+  for (int r = 0; r < c->nranks; ++r) total += counts[r];
+  if (c->rank == root && total && (!xyz_out || !bgr_out))
+    return fail(c, SL_EINVAL, "sl_gather: the root needs output buffers");
+  Rccl* R = rccl();
+  ncclComm_t comm = static_cast<ncclComm_t>(c->comm);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t esz = 3 * (xyz_dtype == SL_XYZ_F64 ? sizeof(double) : sizeof(float));
+  if (c->rank == root) {  // the root's own part: a device copy
+    int64_t off = 0;
+    for (int r = 0; r < root; ++r) off += counts[r];
+    if (n_local) {
+      HIP_TRY(c, hipMemcpyAsync(static_cast<uint8_t*>(xyz_out) + off * esz, xyz, n_local * esz,
+                                hipMemcpyDeviceToDevice, s));
+      HIP_TRY(c, hipMemcpyAsync(bgr_out + 3 * off, bgr, 3 * n_local, hipMemcpyDeviceToDevice, s));
+    }
+  }
+  NCCL_TRY(c, R->group_start());
+  int64_t off = 0;
+  for (int r = 0; r < c->nranks; ++r) {
+    const int64_t n = counts[r];
+    if (c->rank == root && r != root && n) {
+      NCCL_TRY(c, R->recv(static_cast<uint8_t*>(xyz_out) + off * esz, n * esz, ncclUint8, r, comm, s));
+      NCCL_TRY(c, R->recv(bgr_out + 3 * off, 3 * n, ncclUint8, r, comm, s));
+    }
+    off += n;
+  }
+  if (c->rank != root && n_local) {
+    NCCL_TRY(c, R->send(xyz, n_local * esz, ncclUint8, root, comm, s));
+    NCCL_TRY(c, R->send(bgr, 3 * n_local, ncclUint8, root, comm, s));
+  }
+  NCCL_TRY(c, R->group_end());
+  return SL_OK;
+}
+
+const char* sl_last_error(const sl_ctx* c) { return sl_ctx_last_error(c); }
+
+int sl_decode_triangulate_batch(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int n_views, int n_img, int H,
+                                int W, int n_cols, int n_rows, const uint8_t* tex, int64_t tex_vs, int mask_mode,
+                                const double* poses, int32_t* col_out, int32_t* row_out, uint8_t* mask_out,
+                                void* xyz, int xyz_dtype, uint8_t* bgr, int64_t cap, int64_t* view_offsets,
+                                void* stream) {
+  return sl_decode_triangulate(c, stack, stack_vs, n_views, n_img, H, W, n_cols, n_rows, tex, tex_vs, mask_mode,
+                               poses, col_out, row_out, mask_out, xyz, xyz_dtype, bgr, cap, view_offsets, stream);
 }
 
 }  // extern "C"

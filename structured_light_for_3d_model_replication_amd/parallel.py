@@ -75,3 +75,20 @@ def gather_cloud(xyz: torch.Tensor, bgr: torch.Tensor, dst: int = 0, group=None)
     if rank == dst:
         return xyz_all, bgr_all, counts
     return None, None, counts
+
+
+def gather_cloud_native(engine, xyz: torch.Tensor, bgr: torch.Tensor, dst: int = 0, group=None):
+    """gather_cloud through the library's own RCCL communicator (sl_gather,
+    include/slgpu.h) instead of torch.distributed's: rank 0 of ``group`` makes
+    the RCCL unique id, torch.distributed shares it once per engine, then
+    counts and payloads move as in gather_cloud.  Same result and order."""
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    key = (world, rank, id(group))
+    if getattr(engine, "_gather_key", None) != key:
+        uid = [engine.gather_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                   group=group)
+        engine.gather_init(world, rank, uid[0])
+        engine._gather_key = key
+    return engine.gather(xyz, bgr, root=dst)
