@@ -21,6 +21,7 @@ from __future__ import annotations
 import ctypes
 import glob
 import os
+import re
 import threading
 
 import numpy as np
@@ -130,15 +131,32 @@ def postprocess(points, colors, voxel_size: float, nb_neighbors: int = 20, std_r
     return select_by_index(P, C, ind, device=device)
 
 
+def ply_files(folder, order: str = "lexicographic") -> list:
+    """The clouds a 360 merge reads, in its order: ``"lexicographic"`` is
+    processing.py:121's ``sorted(glob('*.ply'))`` (``view_100deg`` before
+    ``view_10deg``); ``"numeric"`` is Old/new360Merge.py:7-20's key, the first
+    integer in the file name (0 when none; ties keep name order)."""
+    if order == "lexicographic":
+        return sorted(glob.glob(os.path.join(folder, "*.ply")))
+    if order == "numeric":
+        names = sorted(f for f in os.listdir(folder) if f.lower().endswith(".ply"))
+
+        def first_int(name):
+            m = re.search(r"\d+", name)
+            return int(m.group()) if m else 0
+        return [os.path.join(folder, f) for f in sorted(names, key=first_int)]
+    raise ValueError("order must be 'lexicographic' or 'numeric'")
+
+
 def merge_pro_360_posed(input_folder, output_path, poses, voxel_size: float = 0.02, *, device=None,
-                        binary: bool = True):
+                        binary: bool = True, order: str = "lexicographic"):
     """merge_pro_360 (processing.py:116-182) with known per-file poses instead
-    of the FPFH/RANSAC/ICP estimate: files ``sorted(glob('*.ply'))`` (the
-    reference's lexicographic order), file i moved by ``poses[i]`` (4x4), merged,
-    post-processed and written (binary PLY, Open3D's default; ``binary=False``
-    for the ASCII format of sl_system.py)."""
+    of the FPFH/RANSAC/ICP estimate: files in ``ply_files(order)`` order
+    (default: the reference's lexicographic one), file i moved by ``poses[i]``
+    (4x4), merged, post-processed and written (binary PLY, Open3D's default;
+    ``binary=False`` for the ASCII format of sl_system.py)."""
     print(f"[Merge 360] Loading clouds from {input_folder}...")
-    files = sorted(glob.glob(os.path.join(input_folder, "*.ply")))
+    files = ply_files(input_folder, order)
     if len(files) < 2:
         raise ValueError("Need at least 2 .ply files to merge.")
     poses = np.asarray(poses, dtype=np.float64).reshape(-1, 4, 4)

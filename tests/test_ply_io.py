@@ -130,3 +130,17 @@ def test_read_ply_ascii_reference_file(name, tmp_path):
     expect = np.array([[float(f"{v:.4f}") for v in p] for p in d["P"]]).reshape(-1, 3)
     np.testing.assert_array_equal(P, expect)
     np.testing.assert_array_equal(C, d["C"])
+
+
+def test_merge_file_orders(tmp_path):
+    """processing.py:121 sorts the per-view clouds lexicographically;
+    Old/new360Merge.py:7-20 by the first integer in the name."""
+    from structured_light_for_3d_model_replication_amd import merge
+    for n in ("view_100deg.ply", "view_10deg.ply", "view_20deg.ply", "view_0deg.ply", "notes.txt", "zz.PLY"):
+        (tmp_path / n).write_text("")
+    lex = [os.path.basename(f) for f in merge.ply_files(str(tmp_path))]
+    num = [os.path.basename(f) for f in merge.ply_files(str(tmp_path), "numeric")]
+    assert lex == ["view_0deg.ply", "view_100deg.ply", "view_10deg.ply", "view_20deg.ply"]
+    assert num == ["view_0deg.ply", "zz.PLY", "view_10deg.ply", "view_20deg.ply", "view_100deg.ply"]
+    with pytest.raises(ValueError):
+        merge.ply_files(str(tmp_path), "mtime")
