@@ -29,6 +29,8 @@
 
 #include <algorithm>
 #include <limits>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "slgpu.h"
@@ -882,13 +884,69 @@ struct PinBuf {
   }
 };
 
+// Scratch pool: the merge entry points allocate several buffers of the
+// cloud's size per call, and hipFree costs ~44 us each (it waits for the
+// device); freed buffers are kept per device (up to kPoolMax bytes) and a
+// request takes the smallest kept buffer of at least its size and at most
+// twice it.  Every buffer returns to the pool only after the stream it was
+// used on has been synchronised (each entry point and helper synchronises
+// before its scratch goes out of scope), so a reused buffer is idle.
+constexpr size_t kPoolMax = size_t{16} << 30;
+
+struct Pool {
+  std::mutex mu;
+  std::multimap<size_t, std::pair<int, void*>> free;  // bytes -> (device, ptr)
+  size_t cached = 0;
+};
+
+Pool& pool() {
+  static Pool* p = new Pool();  // never destroyed: device memory is released with the process
+  return *p;
+}
+
+hipError_t pool_alloc(void** out, size_t bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  {
+    Pool& P = pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (auto it = P.free.lower_bound(bytes); it != P.free.end() && it->first <= 2 * bytes; ++it) {
+      if (it->second.first != dev) continue;
+      *out = it->second.second;
+      P.cached -= it->first;
+      P.free.erase(it);
+      return hipSuccess;
+    }
+  }
+  return hipMalloc(out, bytes);
+}
+
+void pool_free(void* ptr, size_t bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    Pool& P = pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (P.cached + bytes <= kPoolMax) {
+      P.free.emplace(bytes, std::make_pair(dev, ptr));
+      P.cached += bytes;
+      return;
+    }
+  }
+  (void)hipFree(ptr);
+}
+
 template <typename T>
 struct DBuf {
   T* p = nullptr;
+  size_t bytes = 0;
   ~DBuf() {
-    if (p) (void)hipFree(p);
+    if (p) pool_free(p, bytes);
   }
-  hipError_t alloc(int64_t n) { return hipMalloc(reinterpret_cast<void**>(&p), sizeof(T) * std::max<int64_t>(n, 1)); }
+  hipError_t alloc(int64_t n) {
+    bytes = sizeof(T) * static_cast<size_t>(std::max<int64_t>(n, 1));
+    return pool_alloc(reinterpret_cast<void**>(&p), bytes);
+  }
 };
 
 // min / max bound of n points (device) -> host b[6]
