@@ -1,8 +1,10 @@
-"""Kernel-level timing of k_stats / k_decode variants (HIP events), one process.
+"""Kernel-level timing of k_decode / k_count / k_cloud (HIP events around each
+kernel of every call), one process, on a synthetic view (default 4K).
 
-    python scripts/kbench.py [--config c2] [--reps 20]
-Prints one line per variant: mode, k_stats us, k_decode us, algorithmic GB/s.
-Set SLGPU_DEBUG (1 = tile from blockIdx, 2 = no look-back) for ablations.
+    python scripts/kbench.py [--H 2160 --W 3840] [--reps 20] [--only maps+cloud]
+Prints one JSON line per output mode (maps+cloud, cloud, maps, fixed mask):
+kernel microseconds and algorithmic GB/s.  SLGPU_DEBUG selects the
+measurement-only ablations of Params::dbg; SLGPU_LIB a build variant.
 """
 import argparse
 import json
