@@ -124,7 +124,12 @@ def process_views(views, calib_data, *, n_cols=1920, n_rows=1080, device=None, w
     return out
 
 
-def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slots, keep):
+def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slots, keep, mask_mode="fixed",
+                      raise_errors=False):
+    """Views grouped by (frame size, file count), each group through one
+    ``pipeline.ViewPipeline``.  ``raise_errors``: a failing folder raises
+    (SLSystem.generate_clouds) instead of being logged and skipped (the batch
+    GUI's loop)."""
     files = {f: io.list_stack_files(f) for f in views}
     groups: dict = {}
     for f in views:
@@ -134,6 +139,8 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
     failed = set()
 
     def error(f, e):  # the batch loop's per-folder handler (multi_point_cloud_process.py:248-251)
+        if raise_errors:
+            raise e
         failed.add(f)
         log(f"❌ Error in {os.path.basename(f)}: {e}\n")
 
@@ -141,7 +148,7 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
         try:
             eng.set_calibration(calib_data, H, W)
             pipe = pipeline.ViewPipeline(eng, H=H, W=W, n_img=n_img, n_cols=n_cols, n_rows=n_rows,
-                                         mask_mode="fixed", xyz_dtype=torch.float64, slots=slots)
+                                         mask_mode=mask_mode, xyz_dtype=torch.float64, slots=slots)
         except (ValueError, IndexError) as e:
             for f in group:
                 error(f, e)
@@ -151,6 +158,8 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
             try:
                 return io.fill_stack(files[group[i]], stack.numpy(), tex.numpy())
             except (OSError, ValueError) as e:
+                if raise_errors:
+                    raise
                 error(group[i], e)
                 stack[0].zero_()  # white = 0: every pixel masked out, no points
                 return True

@@ -112,3 +112,31 @@ class SLSystem:
         print(f"Saving {len(points)} points to {out_path}...")
         ply.save_ply(points, colors, out_path)
         print(f"[Success] Generated {out_path}")
+
+    def generate_clouds(self, scan_dirs, calib_file, *, slots=3):
+        """Batched ``generate_cloud``: every folder of ``scan_dirs``
+        gets the ``<scan_dir>/<basename>.ply`` that generate_cloud writes for
+        it, byte for byte (adaptive mask, f64 points, sl_system.py:483-694).
+        Views stream through one ``pipeline.ViewPipeline`` per frame size: file
+        decoding, H2D, the kernels and D2H + PLY writing of neighbouring views
+        overlap.  The calibration checks and exceptions are generate_cloud's;
+        a folder with fewer than 4 images raises its ValueError before any
+        view is processed.  Returns the PLY paths in ``scan_dirs`` order."""
+        from . import multi_point_cloud_process as mp
+        if not os.path.exists(calib_file):
+            raise FileNotFoundError(f"Calibration file not found at {calib_file}")
+        data = scipy.io.loadmat(calib_file)
+        if "Oc" not in data:
+            raise ValueError("Calibration file missing 'Oc'.")
+        calib = _to_numpy_calib(data)
+        scan_dirs = [str(d) for d in scan_dirs]
+        for d in scan_dirs:
+            print(f"[Process] Processing {d} using {calib_file}...")
+            if len(io.list_stack_files(d)) < 4:  # sl_system.py:515-516
+                raise ValueError("Not enough images in folder to decode.")
+        mp._process_streamed(scan_dirs, calib, 1920, 1080, self.device, True, print, slots, False,
+                             mask_mode="adaptive", raise_errors=True)
+        outs = [os.path.join(d, os.path.basename(d) + ".ply") for d in scan_dirs]
+        for o in outs:
+            print(f"[Success] Generated {o}")
+        return outs

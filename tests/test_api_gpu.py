@@ -96,3 +96,31 @@ def test_cli_matches_oracle_fixed_mask(tmp_path, capsys):
     assert open(out).read() == o.ply_text(P, C)
     process_cloud.main(["--input", scan, "--output", out, "--calib", str(tmp_path / "nope.mat")])
     assert "Error:" in capsys.readouterr().out
+
+
+def test_generate_clouds_batched_matches_generate_cloud(tmp_path):
+    """SLSystem.generate_clouds: one streamed batch over several folders writes
+    what generate_cloud writes for each (reference PLY for the fixture stack,
+    the oracle's for perturbed stacks of the same rig)."""
+    from oracle import sl_oracle as o
+    from structured_light_for_3d_model_replication_amd.sl_system import SLSystem
+    d = g.load("sl_generate_cloud_e2e")
+    mat = str(tmp_path / "calib.mat")
+    scipy.io.savemat(mat, d["calib"])
+    rng = np.random.default_rng(5)
+    base = d["stack"].astype(np.int16)
+    stacks = [d["stack"],
+              np.clip(base + rng.integers(-12, 13, base.shape), 0, 255).astype(np.uint8),
+              np.concatenate([d["stack"][:1] // 2, d["stack"][1:]])]
+    dirs = [_scan(tmp_path / f"view_{k}", s) for k, s in enumerate(stacks)]
+    outs = SLSystem().generate_clouds(dirs, mat, slots=2)
+    assert outs == [os.path.join(f, os.path.basename(f) + ".ply") for f in dirs]
+    assert open(outs[0]).read() == g.ply_text(d["meta"]["ply"])
+    for s, out in zip(stacks, outs):
+        P, C = o.decode_triangulate(list(s), None, d["calib"], 1920, 1080)[3:]
+        assert open(out).read() == o.ply_text(P, C)
+    few = _scan(tmp_path / "few", d["stack"][:3])
+    with pytest.raises(ValueError, match="Not enough images"):
+        SLSystem().generate_clouds([dirs[0], few], mat)
+    with pytest.raises(FileNotFoundError):
+        SLSystem().generate_clouds(dirs, str(tmp_path / "missing.mat"))
