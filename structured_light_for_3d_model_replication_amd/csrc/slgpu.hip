@@ -366,6 +366,10 @@ __device__ __forceinline__ bool has_point(const Params& p, int mode, const float
 //            banks, added to the view's global histogram once per workgroup.
 // Grid (chunk groups, views); waves past the view's last chunk run empty (the
 // workgroup barriers count them).
+#ifndef SLGPU_DECODE_PER_CU
+#define SLGPU_DECODE_PER_CU 2
+#endif
+constexpr int kDecodePerCu = SLGPU_DECODE_PER_CU;  // default k_decode grid cap, workgroups per CU (0: none)
 #ifndef SLGPU_DECODE_WAVES
 #define SLGPU_DECODE_WAVES 1
 #endif
@@ -384,13 +388,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
-  const int civ = blockIdx.x * kWaves + wid;  // chunk in view
-  const bool live = civ < p.cpv;
   const int64_t HW = p.HW;
-  const int64_t px0 = static_cast<int64_t>(civ) * kChunk + lane * kPx;
-  const int n_px = live ? static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx)) : 0;
-  const int64_t pxl = n_px > 0 ? px0 : 0;  // keep loads unconditional and in bounds
-  const int64_t o = view * HW + px0;
 
   // the next launch's histogram (scratch of this one)
   if (hist && blockIdx.x == 0)
@@ -399,6 +397,19 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
     for (int i = tid; i < 256 * kHistStride; i += kThreads) s_hist[i] = 0u;
     __syncthreads();
   }
+
+  // Chunk groups of the view, strided over the grid's x (one group per
+  // workgroup unless the launch caps the grid, SLGPU_DECODE_GRID); the
+  // workgroup-uniform loop holds no barrier.
+  const int ngroups = (p.cpv + kWaves - 1) / kWaves;
+  int mx_acc = -1024;
+  for (int cg = blockIdx.x; cg < ngroups; cg += gridDim.x) {
+  const int civ = cg * kWaves + wid;  // chunk in view
+  const bool live = civ < p.cpv;
+  const int64_t px0 = static_cast<int64_t>(civ) * kChunk + lane * kPx;
+  const int n_px = live ? static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx)) : 0;
+  const int64_t pxl = n_px > 0 ? px0 : 0;  // keep loads unconditional and in bounds
+  const int64_t o = view * HW + px0;
 
   uint32_t col[kPx];
   if (mode & M_FROMMAPS) {
@@ -547,9 +558,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
           mx = max(mx, static_cast<int>(byte_of(wq, k)) - bk);
         }
       }
-#pragma unroll
-      for (int d = 32; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
-      if (lane == 0) s_max[wid] = mx;
+      mx_acc = max(mx_acc, mx);
     }
   }
 
@@ -572,8 +581,12 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         if (k < n_px) p.codes[o + k] = static_cast<uint16_t>(rec[k >> 1] >> (16 * (k & 1)));
     }
   }
+  }  // chunk groups
 
   if (hist) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) mx_acc = max(mx_acc, __shfl_xor(mx_acc, d, 64));
+    if (lane == 0) s_max[wid] = mx_acc;
     __syncthreads();
     unsigned* gh = p.hist + view * kSlot;
     unsigned cnt = 0u;
@@ -1305,6 +1318,7 @@ struct sl_ctx {
   int64_t cap_codes = 0;
   int last_views = 0;
   int dbg = 0;
+  int decode_wgs = 0;  // k_decode grid cap in workgroups over all views (0: one workgroup per chunk group)
   // optional per-call HIP-event timing of k_decode / k_count / k_cloud
   std::vector<hipEvent_t> prof_ev;  // kProfEv events per call slot
   std::vector<int> prof_groups;     // launch groups recorded per call
@@ -1319,7 +1333,7 @@ struct sl_ctx {
     bool valid = false;
     Params p[3];
     const void* fn[3] = {nullptr, nullptr, nullptr};  // k_decode, k_count, k_cloud (or null)
-    dim3 grid;
+    dim3 grid[3];
     hipStream_t s = nullptr;
   } last;
 };
@@ -1513,7 +1527,10 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     }
     const dim3 grid(static_cast<unsigned>((cpv + kWaves - 1) / kWaves), static_cast<unsigned>(nv));
     c->last.valid = true;
-    c->last.grid = grid;
+    dim3 dgrid = grid;  // k_decode: chunk groups strided over a capped grid
+    if (c->decode_wgs > 0) dgrid.x = std::min(grid.x, static_cast<unsigned>(std::max(1, (c->decode_wgs + nv - 1) / nv)));
+    c->last.grid[0] = dgrid;
+    c->last.grid[1] = c->last.grid[2] = grid;
     c->last.s = s;
     c->last.fn[2] = nullptr;
     {
@@ -1522,7 +1539,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       KernelFn fn = pick_decode(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode, vec);
       c->last.p[0] = p;
       c->last.fn[0] = reinterpret_cast<const void*>(fn);
-      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(kThreads), args, 0, s));
+      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dgrid, dim3(kThreads), args, 0, s));
     }
     if (gev) HIP_TRY(c, hipEventRecord(gev[1], s));
     {
@@ -1681,6 +1698,12 @@ int sl_ctx_create(int device, sl_ctx** out) {
     delete c;
     return SL_EHIP;
   }
+  // k_decode workgroups per CU when its grid is capped (SLGPU_DECODE_PER_CU,
+  // default kDecodePerCu; 0 = uncapped)
+  int per_cu = kDecodePerCu, n_cu = 0;
+  if (const char* d = getenv("SLGPU_DECODE_PER_CU")) per_cu = atoi(d);
+  if (per_cu > 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
+    c->decode_wgs = per_cu * n_cu;
   *out = c;
   return SL_OK;
 }
@@ -1998,7 +2021,7 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
       Params p = c->last.p[k];
       void* args[] = {&p};
       for (int i = 0; i < reps; ++i) {
-        const hipError_t e = hipLaunchKernel(c->last.fn[k], c->last.grid, dim3(kThreads), args, 0, s);
+        const hipError_t e = hipLaunchKernel(c->last.fn[k], c->last.grid[k], dim3(kThreads), args, 0, s);
         if (e != hipSuccess) {
           r = fail(c, SL_EHIP, std::string("sl_time_kernels: ") + hipGetErrorString(e));
           break;
