@@ -120,7 +120,10 @@ constexpr int kSlot = 272;                 // histogram of one view: 256 bins + 
 constexpr int kHistRep = 32;               // LDS histogram replicas (one per lane of a half-wave)
 constexpr int kHistStride = kHistRep + 1;  // bin stride: replica r of bin b sits in bank (b + r) % 32
 constexpr int kMaxWp = 32768;              // projector columns (record codes are 15 bits)
-constexpr int64_t kMaxChunks = 1 << 14;    // chunks per launch group: bounds k_cloud's prefix reads
+#ifndef SLGPU_MAX_CHUNKS
+#define SLGPU_MAX_CHUNKS (1 << 14)
+#endif
+constexpr int64_t kMaxChunks = SLGPU_MAX_CHUNKS;  // chunks per launch group: bounds k_cloud's prefix reads
 
 struct ViewStats {
   int thr_white;        // mask: white > thr_white
