@@ -165,9 +165,11 @@ def main():
     for _ in range(a.steps):
         step(out)
     torch.cuda.synchronize(dev)
+    # this rank's K steps are complete here; the closing barrier's own latency
+    # stays out of the interval (the max over ranks below covers rank skew)
+    el = time.perf_counter() - t0
     if distributed:
         dist.barrier()
-    el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
