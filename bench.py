@@ -54,9 +54,16 @@ XYZ_MODES = {True: "SL_XYZ_F32_FAST: f32 arithmetic, per-coordinate rel err <= 1
              False: "SL_XYZ_F32: f64 arithmetic, xyz = correctly rounded float32 of the reference's f64"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks) of one node; without torch.distributed.run, N > 1 starts N ranks itself")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: the config's views per GPU; strong: the config's views in total, sharded")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend (gloo only with --selftest)")
+    ap.add_argument("--selftest", action="store_true",
+                    help="CPU plumbing test of the launcher / timing / gather (no GPU, no kernels)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
@@ -69,7 +76,77 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per k_decode launch (from profiles/)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a) -> int:
+    """``--gpus N`` run without torch.distributed.run: start the N ranks (one
+    process per GPU) as a child ``torch.distributed.run`` on 127.0.0.1 and
+    return its exit status.  This process touches no GPU (the ranks do), and it
+    starts the launcher as a child, not by exec."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def rank_env():
+    """(world, rank, local_rank, distributed) from torch.distributed.run's env."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
+    return world, rank, local, distributed
+
+
+def selftest(a) -> None:
+    """CPU plumbing test of the multi-rank bench (``--selftest --backend gloo``):
+    the same launch, barrier + max-over-ranks timing and rank-order gather as
+    the GPU bench, with a stand-in per-rank cloud of known size instead of the
+    kernels (the kernels' parity is the GPU tests' job).  Rank 0 prints one
+    JSON line with n_gpus and the gathered point count."""
+    world, rank, _, distributed = rank_env()
+    if distributed:
+        dist.init_process_group("gloo")
+    V = a.views or 3
+    views = list(parallel.shard_views(V * world, world, rank)) if a.scaling == "weak" else \
+        list(parallel.shard_views(V, world, rank))
+    n_per_view = 1000
+    if distributed:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        xyz = torch.cat([torch.full((n_per_view, 3), float(v), dtype=torch.float32) for v in views]) \
+            if views else torch.zeros((0, 3), dtype=torch.float32)
+        bgr = torch.zeros((xyz.shape[0], 3), dtype=torch.uint8)
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64)
+    if distributed:
+        dist.barrier()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        xa, _, counts = parallel.gather_cloud(xyz, bgr, dst=0)
+    else:
+        xa, counts = xyz, [xyz.shape[0]]
+    if rank == 0:
+        order_ok = bool(torch.equal(xa[::n_per_view, 0], torch.arange(xa.shape[0] // n_per_view,
+                                                                      dtype=torch.float32)))
+        print(json.dumps({"metric": "selftest", "n_gpus": world, "steps": a.steps, "scaling": a.scaling,
+                          "views_total": V * world if a.scaling == "weak" else V,
+                          "gathered_points": int(xa.shape[0]), "counts": counts, "view_order_ok": order_ok,
+                          "max_rank_s": float(t.item())}))
+    if distributed:
+        dist.destroy_process_group()
 
 
 def path_bytes(H, W, read_planes, n_points, maps):
@@ -106,12 +183,17 @@ def cpu_baseline(stack_h, tex_h, calib, budget_s):
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # launched by torch.distributed.run (any world size, 1 included): RCCL process
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))  # this process never touches a GPU
+    # launched by torch.distributed.run (any world size, 1 included): process
     # group, barrier + max-over-ranks timing and the gather all run
-    distributed = world > 1 or ("RANK" in os.environ and "MASTER_ADDR" in os.environ)
+    world, rank, local, distributed = rank_env()
+    if "WORLD_SIZE" in os.environ and world != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} disagrees with WORLD_SIZE={world}")
+    if a.selftest:
+        return selftest(a)
+    if a.backend != "nccl":
+        sys.exit("bench.py: --backend gloo is only for --selftest (the GPU bench gathers over RCCL)")
     if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -119,7 +201,16 @@ def main():
     torch.cuda.set_device(dev)
     cfg = CONFIGS[a.config]
     H, W, Wp, Hp, rows, maps = cfg["H"], cfg["W"], cfg["Wp"], cfg["Hp"], cfg["rows"], cfg["maps"]
-    V = a.views or cfg["views"]
+    V_cfg = a.views or cfg["views"]
+    if a.scaling == "strong":
+        # the config's views in total, sharded in contiguous blocks over the ranks
+        if V_cfg < world:
+            sys.exit(f"bench.py: --scaling strong needs at least {world} views (got {V_cfg})")
+        my_views = list(parallel.shard_views(V_cfg, world, rank))
+    else:
+        my_views = [rank * V_cfg + v for v in range(V_cfg)]  # V_cfg per GPU, contiguous blocks
+    V = len(my_views)
+    V_total = V_cfg if a.scaling == "strong" else V_cfg * world
     rig = synth.Rig(H=H, W=W, Wp=Wp, Hp=Hp)
     calib = synth.make_calibration(rig, with_Nc=False)
     cfg_idx = int(a.config[1:])
@@ -127,7 +218,7 @@ def main():
     tex = torch.empty((V, H, W, 3), dtype=torch.uint8, device=dev)
     poses = torch.empty((V, 4, 4), dtype=torch.float64, device=dev) if cfg["pose"] else None
     for v in range(V):
-        gv = rank * V + v  # global view index: views sharded in contiguous blocks
+        gv = my_views[v]  # global view index
         s, t = synth.render_stack(rig, seed=1000 * cfg_idx + gv, include_rows=rows,
                                   view_deg=cfg["deg"] * gv, device=dev)
         if stack is None:
@@ -224,7 +315,7 @@ def main():
             step(out3, fast=not head_fast)
         _, _, acloud_ms, anl = eng.profile_read()
         eng.sync()
-        alt = {"xyz_mode": XYZ_MODES[not head_fast], "px_per_s": world * V * H * W * a.steps / el_alt,
+        alt = {"xyz_mode": XYZ_MODES[not head_fast], "px_per_s": V_total * H * W * a.steps / el_alt,
                "ms_per_step": 1e3 * el_alt / a.steps, "k_cloud_ms": acloud_ms / max(anl, 1)}
         del out3
 
@@ -241,8 +332,8 @@ def main():
         gather_ms = 1e3 * float(gt.item())
 
     if rank == 0:
-        px_step = V * H * W
-        value = world * px_step * a.steps / el
+        px_step = V_total * H * W  # whole job: every rank's views
+        value = px_step * a.steps / el
         # the re-run figure only where the group's stack exceeds the 256 MB
         # Infinity Cache (else the re-runs would read it warm): in-step events
         rerun_ok = H * W * read_planes * v_last > 256 * 2 ** 20
@@ -276,15 +367,15 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": 1e3 * el / a.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "u8+f32" if head_fast else "u8+f64",
             "data": "synthetic",
-            "config": {"workload": f"BASELINE config {cfg_idx}: {V} x {W}x{H} view(s) per GPU per step, "
+            "config": {"workload": f"BASELINE config {cfg_idx}: {V} x {W}x{H} view(s) per GPU per step ({a.scaling} scaling, {V_total} in all), "
                                    f"{n_planes}-plane stacks (Gray {nc}+{n_planes // 2 - 1 - nc} bits + inverses), "
                                    + ("col/row/mask maps + " if maps else "")
                                    + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
-                       "views_per_gpu": V, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
+                       "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
                        "parallelism": f"views sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -305,7 +396,7 @@ def main():
                                                      "inputs fit the 256 MB Infinity Cache, so theirs run warm"}},
             "cpu_baseline": cpu,
             "points_per_view": n_pts / V,
-            "cloud_only_px_per_s": None if el_cloud is None else world * px_step * a.steps / el_cloud,
+            "cloud_only_px_per_s": None if el_cloud is None else px_step * a.steps / el_cloud,
             "gather_ms": gather_ms,
             "xyz_mode": XYZ_MODES[head_fast],
             "alt_xyz_mode": alt,

@@ -207,6 +207,11 @@ int sl_select_by_index(sl_ctx* ctx, const double* xyz, const uint8_t* bgr, const
  * ((m0 x + m1 y) + m2 z) + m3 -- PointCloud::Transform.  Asynchronous. */
 int sl_transform_points(sl_ctx* ctx, double* xyz, int64_t n, const double* pose, void* stream);
 
+/* Release the scratch buffers the merge entry points keep pooled for `device`
+ * (kept otherwise for the process's lifetime, at most 16 GiB per device);
+ * the bytes released -> *released_bytes (may be NULL). */
+int sl_merge_pool_trim(int device, int64_t* released_bytes);
+
 /* ---- multi-GPU gather ----
  * The merge's one exchange: every rank's cloud to `root` in rank order over
  * RCCL (opened with dlopen by soname, so a process that already holds

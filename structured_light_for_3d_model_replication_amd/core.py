@@ -75,6 +75,16 @@ def calibration_arrays(calib: dict, H: int, W: int):
     return _f64c(calib["cam_K"]).reshape(3, 3), Oc, _f64c(planes[:, :4]), None if Nc is None else _f64c(Nc)
 
 
+def _hasher():
+    """A 128-bit content hash: xxh3 (~20 GB/s: a 4K camera's 199 MB Nc in ~10
+    ms) where the xxhash module is installed, else blake2b."""
+    try:
+        import xxhash
+        return xxhash.xxh3_128()
+    except ImportError:
+        return hashlib.blake2b(digest_size=16)
+
+
 def _xyz_code(xyz_dtype, fast_f32: bool) -> int:
     if xyz_dtype == torch.float64:
         if fast_f32:
@@ -117,12 +127,13 @@ class Reconstructor:
     # ------------------------------------------------------------ calibration
     def set_calibration(self, calib: dict, H: int, W: int) -> None:
         K, Oc, planes, Nc = calibration_arrays(calib, H, W)
-        h = hashlib.blake2b(digest_size=16)
-        for a in (K, Oc, planes):
-            h.update(a.tobytes())
-        if Nc is not None:
-            h.update(Nc[:, :: max(1, Nc.shape[1] // 4096)].tobytes())
-            h.update(str(id(calib.get("Nc"))).encode())
+        # content key over every byte of the calibration (the full Nc table
+        # included: no sampling, no object identity), so a changed or reused
+        # array always re-uploads
+        h = _hasher()
+        for a in (K, Oc, planes) + (() if Nc is None else (Nc,)):
+            h.update(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
+            h.update(str(a.shape).encode())
         key = (H, W, h.hexdigest(), Nc is None)
         with self._lock:
             if key == self._calib_key:

@@ -119,6 +119,16 @@ constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
 constexpr int kSlot = 272;                 // histogram of one view: 256 bins + max + pad (u32)
 constexpr int kHistRep = 32;               // LDS histogram replicas (one per lane of a half-wave)
 constexpr int kHistStride = kHistRep + 1;  // bin stride: replica r of bin b sits in bank (b + r) % 32
+// Measurement-only ablations, compiled in only by -DSLGPU_ABLATE=<bits> (a
+// separate build for scripts/, never the shipped library): 1 = k_cloud without
+// point math, 2 = k_cloud without xyz/colour stores, 4 = k_cloud without
+// operand gathers, 8 = k_cloud stops after its loads + rank scan, 16 = ... after
+// the LDS compaction, 32 = k_count with the fixed thresholds, 64 = k_count
+// without the |n.r| test, 128 = k_count without plane gathers.
+#ifndef SLGPU_ABLATE
+#define SLGPU_ABLATE 0
+#endif
+constexpr int kAblate = SLGPU_ABLATE;
 constexpr int kMaxWp = 32768;              // projector columns (record codes are 15 bits)
 #ifndef SLGPU_MAX_CHUNKS
 #define SLGPU_MAX_CHUNKS (1 << 14)
@@ -149,11 +159,6 @@ struct Params {
   int64_t n_chunks;  // n_views * cpv
   int nc, nr, kc, kr;  // code bits and available bit planes (pairs)
   int mode;
-  int dbg;  // measurement-only ablations (SLGPU_DEBUG env): 1 = k_cloud without point math,
-            // 2 = k_cloud without xyz/colour stores, 4 = k_cloud without operand gathers,
-            // 8 = k_cloud stops after its loads + rank scan, 16 = ... after the LDS compaction,
-            // 32 = k_count with the fixed thresholds, 64 = k_count without the |n.r| test,
-            // 128 = k_count without plane gathers, 256 = k_count without super-block atomics
   int Wp;
   const double4* planes;   // (n0, n1, n2, num = n.Oc + d) per projector column
   const float4* planes32;  // f32 (n0, n1, n2, -) for the point/no-point pre-decision
@@ -633,7 +638,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
   // scan then waits for it alone), then the chunk ----
   uint4 hb = make_uint4(0u, 0u, 0u, 0u);
   unsigned hmax = 0u;
-  const bool adaptive = (mode & M_HIST) && !(p.dbg & 32);
+  const bool adaptive = (mode & M_HIST) && !(kAblate & 32);
   if (adaptive) {
     const unsigned* h = p.hist + view * kSlot;
     hb = reinterpret_cast<const uint4*>(h)[lane];
@@ -773,7 +778,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const unsigned c = (rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu;
-        pf[e] = (p.dbg & 128) ? make_float4(0.5f, 0.25f, 1.0f + 1e-3f * c, 0.0f) : p.planes32[c];
+        pf[e] = (kAblate & 128) ? make_float4(0.5f, 0.25f, 1.0f + 1e-3f * c, 0.0f) : p.planes32[c];
       }
       ys = 0.0f;
       if (!nc) {
@@ -799,7 +804,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
     // table's largest sum|n_i| (sl_set_calib, rounded up): one compare per
     // pixel.  Masked pixels that fail it take the bounded test below.
     uint32_t todo = ok[s];
-    if (p.dbg & 64) {
+    if (kAblate & 64) {
       nib = todo;
       todo = 0u;
     } else if (vec && !nc) {
@@ -972,7 +977,7 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   const int incl = wave_incl_scan(n_l, lane);
   const int total = __shfl(incl, 63, 64);
   if (lane == 0 && civ == 0) p.view_offsets[view] = base;
-  if (p.dbg & 8) {  // measurement only: stop after the loads and the rank scan
+  if (kAblate & 8) {  // measurement only: stop after the loads and the rank scan
     if (total == -1) p.bgr[0] = static_cast<uint8_t>(d[0] ^ tq[0].x ^ tq[1].y ^ tq[2].z);
     return;
   }
@@ -1010,7 +1015,7 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
     }
   }
   __builtin_amdgcn_wave_barrier();
-  if (p.dbg & 16) return;  // measurement only: stop after the LDS compaction
+  if (kAblate & 16) return;  // measurement only: stop after the LDS compaction
 
   cloud_points<MODE>(p, view, cpx, base, lane, total, s_ent, s_bgr, s_sxyz, s_scol);
 }
@@ -1033,7 +1038,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
   const int v_c = static_cast<int>(cpx / W);
   const double* pose = p.poses ? p.poses + 16 * view : nullptr;
   const bool f64out = (mode & M_XYZ64) != 0;
-  const int dbg = p.dbg;
+  constexpr int dbg = kAblate;
   auto point_bgr = [&](int j, int local) -> uint32_t {
     if (kLdsBgr) return s_bgr[j];
     if (kTexLds) {
@@ -1320,7 +1325,6 @@ struct sl_ctx {
   uint16_t* d_codes = nullptr;  // k_decode -> k_count / k_cloud records
   int64_t cap_codes = 0;
   int last_views = 0;
-  int dbg = 0;
   int decode_wgs = 0;  // k_decode grid cap in workgroups over all views (0: one workgroup per chunk group)
   // optional per-call HIP-event timing of k_decode / k_count / k_cloud
   std::vector<hipEvent_t> prof_ev;  // kProfEv events per call slot
@@ -1696,7 +1700,6 @@ int sl_ctx_create(int device, sl_ctx** out) {
   *out = nullptr;
   sl_ctx* c = new sl_ctx();
   c->device = device;
-  if (const char* d = getenv("SLGPU_DEBUG")) c->dbg = atoi(d);  // measurement-only ablations
   if (hipSetDevice(device) != hipSuccess) {
     delete c;
     return SL_EHIP;
@@ -1866,7 +1869,6 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.o0 = c->Oc[0];
   p.o1 = c->Oc[1];
   p.o2 = c->Oc[2];
-  p.dbg = c->dbg;
 }
 
 int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int n_views, int n_img,
@@ -2220,21 +2222,34 @@ int sl_gather(sl_ctx* c, const void* xyz, int xyz_dtype, const uint8_t* bgr, con
       HIP_TRY(c, hipMemcpyAsync(bgr_out + 3 * off, bgr, 3 * n_local, hipMemcpyDeviceToDevice, s));
     }
   }
+  // Inside the group every failure is recorded and the group is still closed:
+  // an open group would capture this thread's later RCCL calls (torch's too,
+  // the library handle is shared).
   NCCL_TRY(c, R->group_start());
+  ncclResult_t first = ncclSuccess;
+  const char* what = "";
+  auto rec = [&](ncclResult_t e, const char* op) {
+    if (e != ncclSuccess && first == ncclSuccess) {
+      first = e;
+      what = op;
+    }
+  };
   int64_t off = 0;
-  for (int r = 0; r < c->nranks; ++r) {
+  for (int r = 0; r < c->nranks && first == ncclSuccess; ++r) {
     const int64_t n = counts[r];
     if (c->rank == root && r != root && n) {
-      NCCL_TRY(c, R->recv(static_cast<uint8_t*>(xyz_out) + off * esz, n * esz, ncclUint8, r, comm, s));
-      NCCL_TRY(c, R->recv(bgr_out + 3 * off, 3 * n, ncclUint8, r, comm, s));
+      rec(R->recv(static_cast<uint8_t*>(xyz_out) + off * esz, n * esz, ncclUint8, r, comm, s), "ncclRecv(xyz)");
+      if (first == ncclSuccess) rec(R->recv(bgr_out + 3 * off, 3 * n, ncclUint8, r, comm, s), "ncclRecv(bgr)");
     }
     off += n;
   }
-  if (c->rank != root && n_local) {
-    NCCL_TRY(c, R->send(xyz, n_local * esz, ncclUint8, root, comm, s));
-    NCCL_TRY(c, R->send(bgr, 3 * n_local, ncclUint8, root, comm, s));
+  if (c->rank != root && n_local && first == ncclSuccess) {
+    rec(R->send(xyz, n_local * esz, ncclUint8, root, comm, s), "ncclSend(xyz)");
+    if (first == ncclSuccess) rec(R->send(bgr, 3 * n_local, ncclUint8, root, comm, s), "ncclSend(bgr)");
   }
-  NCCL_TRY(c, R->group_end());
+  const ncclResult_t ge = R->group_end();
+  if (first != ncclSuccess) return fail(c, SL_EHIP, std::string(what) + ": " + R->error_string(first));
+  if (ge != ncclSuccess) return fail(c, SL_EHIP, std::string("ncclGroupEnd: ") + R->error_string(ge));
   return SL_OK;
 }
 

@@ -886,23 +886,34 @@ struct PinBuf {
 
 // Scratch pool: the merge entry points allocate several buffers of the
 // cloud's size per call, and hipFree costs ~44 us each (it waits for the
-// device); freed buffers are kept per device (up to kPoolMax bytes) and a
-// request takes the smallest kept buffer of at least its size and at most
-// twice it.  Every buffer returns to the pool only after the stream it was
-// used on has been synchronised (each entry point and helper synchronises
-// before its scratch goes out of scope), so a reused buffer is idle.
-constexpr size_t kPoolMax = size_t{16} << 30;
+// device); freed buffers are kept per device (up to kPoolMax bytes per device)
+// and a request takes the smallest kept buffer of that device of at least its
+// size and at most twice it.  A buffer goes back to the pool only once the
+// stream it was used on is idle: DBuf remembers the stream of its entry point
+// (PoolStream) and synchronises it when the scope ends, on the error returns
+// too, so a reused buffer is never still in use by a queued kernel (on the
+// normal path the stream is already synchronised and the extra wait is free).
+// sl_merge_pool_trim releases a device's kept buffers.
+constexpr size_t kPoolMax = size_t{16} << 30;  // per device
 
 struct Pool {
   std::mutex mu;
   std::multimap<size_t, std::pair<int, void*>> free;  // bytes -> (device, ptr)
-  size_t cached = 0;
+  std::map<int, size_t> cached;                       // device -> kept bytes
 };
 
 Pool& pool() {
   static Pool* p = new Pool();  // never destroyed: device memory is released with the process
   return *p;
 }
+
+thread_local hipStream_t tls_stream = nullptr;  // the running entry point's stream
+
+struct PoolStream {  // RAII: the stream the entry point's scratch is used on
+  hipStream_t prev;
+  explicit PoolStream(hipStream_t s) : prev(tls_stream) { tls_stream = s; }
+  ~PoolStream() { tls_stream = prev; }
+};
 
 hipError_t pool_alloc(void** out, size_t bytes) {
   int dev = 0;
@@ -914,7 +925,7 @@ hipError_t pool_alloc(void** out, size_t bytes) {
     for (auto it = P.free.lower_bound(bytes); it != P.free.end() && it->first <= 2 * bytes; ++it) {
       if (it->second.first != dev) continue;
       *out = it->second.second;
-      P.cached -= it->first;
+      P.cached[dev] -= it->first;
       P.free.erase(it);
       return hipSuccess;
     }
@@ -922,29 +933,55 @@ hipError_t pool_alloc(void** out, size_t bytes) {
   return hipMalloc(out, bytes);
 }
 
+// ptr must be idle (its stream synchronised)
 void pool_free(void* ptr, size_t bytes) {
   int dev = 0;
   if (hipGetDevice(&dev) == hipSuccess) {
     Pool& P = pool();
     std::lock_guard<std::mutex> lk(P.mu);
-    if (P.cached + bytes <= kPoolMax) {
+    if (P.cached[dev] + bytes <= kPoolMax) {
       P.free.emplace(bytes, std::make_pair(dev, ptr));
-      P.cached += bytes;
+      P.cached[dev] += bytes;
       return;
     }
   }
   (void)hipFree(ptr);
 }
 
+size_t pool_trim(int dev) {
+  std::vector<void*> drop;
+  size_t bytes = 0;
+  {
+    Pool& P = pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (auto it = P.free.begin(); it != P.free.end();) {
+      if (it->second.first == dev) {
+        drop.push_back(it->second.second);
+        bytes += it->first;
+        it = P.free.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    P.cached[dev] = 0;
+  }
+  for (void* p : drop) (void)hipFree(p);
+  return bytes;
+}
+
 template <typename T>
 struct DBuf {
   T* p = nullptr;
   size_t bytes = 0;
+  hipStream_t s = nullptr;
   ~DBuf() {
-    if (p) pool_free(p, bytes);
+    if (!p) return;
+    (void)hipStreamSynchronize(s);  // idle before reuse (an early error return may leave work queued)
+    pool_free(p, bytes);
   }
   hipError_t alloc(int64_t n) {
     bytes = sizeof(T) * static_cast<size_t>(std::max<int64_t>(n, 1));
+    s = tls_stream;
     return pool_alloc(reinterpret_cast<void**>(&p), bytes);
   }
 };
@@ -1087,6 +1124,7 @@ int sl_voxel_downsample(sl_ctx* c, const double* xyz, const uint8_t* bgr, int64_
   *out_n = 0;
   if (n == 0) return SL_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  PoolStream pool_stream(s);
   MTRY(c, hipSetDevice(slgpu_device(c)));
   double b[6];
   int r = bounds(c, xyz, n, b, s);
@@ -1127,6 +1165,7 @@ int sl_statistical_outliers(sl_ctx* c, const double* xyz, int64_t n, int nb_neig
   *out_n = 0;
   if (n == 0) return SL_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  PoolStream pool_stream(s);
   MTRY(c, hipSetDevice(slgpu_device(c)));
   double b[6];
   int r = bounds(c, xyz, n, b, s);
@@ -1372,6 +1411,17 @@ int sl_transform_points(sl_ctx* c, double* xyz, int64_t n, const double* pose, v
   MTRY(c, hipSetDevice(slgpu_device(c)));
   hipLaunchKernelGGL(k_transform, dim3(blocks(n)), dim3(kT), 0, static_cast<hipStream_t>(stream), xyz, n, pose);
   MTRY(c, hipGetLastError());
+  return SL_OK;
+}
+
+// Release the scratch buffers the merge pool keeps for `device` (they are
+// otherwise kept for the process's lifetime, up to 16 GiB per device).
+int sl_merge_pool_trim(int device, int64_t* released_bytes) {
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return SL_EHIP;
+  const size_t b = pool_trim(device);
+  (void)hipSetDevice(prev);
+  if (released_bytes) *released_bytes = static_cast<int64_t>(b);
   return SL_OK;
 }
 

@@ -123,6 +123,15 @@ def transform(points, pose, *, device=None) -> torch.Tensor:
     return P
 
 
+def pool_trim(device=None) -> int:
+    """Release the merge kernels' pooled scratch buffers of ``device``
+    (sl_merge_pool_trim); returns the bytes released."""
+    eng = _engine(device)
+    out = ctypes.c_int64()
+    _lib.check(eng._L.sl_merge_pool_trim(eng.device.index, ctypes.byref(out)), None, "sl_merge_pool_trim")
+    return out.value
+
+
 def postprocess(points, colors, voxel_size: float, nb_neighbors: int = 20, std_ratio: float = 2.0, *,
                 device=None):
     """processing.py:171-175: voxel_down_sample, then remove_statistical_outlier + select_by_index."""

@@ -43,12 +43,16 @@ def gather_cloud(xyz: torch.Tensor, bgr: torch.Tensor, dst: int = 0, group=None)
 
     Returns ``(xyz_all, bgr_all, counts)`` on ``dst`` and ``(None, None, counts)``
     elsewhere.  Payloads move rank -> dst directly (batched isend/irecv).
+    ``dst`` and the ranks are those of ``group`` (default: the world).
     """
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     xyz = xyz.contiguous()
     bgr = bgr.contiguous()
     counts = gather_counts(xyz.shape[0], xyz.device, group)
+
+    def peer(r):  # P2POp peers are global ranks; r and dst are ranks of `group`
+        return r if group is None else dist.get_global_rank(group, r)
     if world == 1:
         return xyz, bgr, counts
     ops = []
@@ -63,12 +67,12 @@ def gather_cloud(xyz: torch.Tensor, bgr: torch.Tensor, dst: int = 0, group=None)
                 xyz_all[off:off + n].copy_(xyz)
                 bgr_all[off:off + n].copy_(bgr)
             elif n:
-                ops.append(dist.P2POp(dist.irecv, xyz_all[off:off + n], r, group))
-                ops.append(dist.P2POp(dist.irecv, bgr_all[off:off + n], r, group))
+                ops.append(dist.P2POp(dist.irecv, xyz_all[off:off + n], peer(r), group))
+                ops.append(dist.P2POp(dist.irecv, bgr_all[off:off + n], peer(r), group))
             off += n
     elif counts[rank]:
-        ops.append(dist.P2POp(dist.isend, xyz, dst, group))
-        ops.append(dist.P2POp(dist.isend, bgr, dst, group))
+        ops.append(dist.P2POp(dist.isend, xyz, peer(dst), group))
+        ops.append(dist.P2POp(dist.isend, bgr, peer(dst), group))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()

@@ -1,0 +1,46 @@
+"""bench.py's multi-rank launch, on CPU (gloo): ``--gpus N`` without
+torch.distributed.run must start N ranks itself, report n_gpus == N and gather
+every rank's cloud to rank 0 in view order (``--selftest``: the launch, timing
+and gather plumbing with a stand-in per-rank cloud, no kernels)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, env=env, cwd=REPO)
+    return p
+
+
+def _json_line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n,scaling,views,expect", [(2, "weak", 3, 6000), (3, "strong", 7, 7000)])
+def test_gpus_n_starts_n_ranks(n, scaling, views, expect):
+    p = _run(["--gpus", str(n), "--selftest", "--backend", "gloo", "--steps", "2", "--scaling", scaling,
+              "--views", str(views)])
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = _json_line(p.stdout)
+    assert r["n_gpus"] == n
+    assert r["gathered_points"] == expect
+    assert sum(r["counts"]) == expect and len(r["counts"]) == n
+    assert r["view_order_ok"]
+
+
+def test_gpus_disagreeing_with_world_size_is_an_error():
+    p = _run(["--gpus", "2", "--selftest", "--backend", "gloo", "--steps", "1"],
+             {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0
+    assert "disagrees with WORLD_SIZE" in p.stderr

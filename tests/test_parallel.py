@@ -84,3 +84,41 @@ def test_gather_cloud_gloo_world2(V):
     np.testing.assert_array_equal(xa, np.concatenate([r[0] for r in ref]))
     np.testing.assert_array_equal(ca, np.concatenate([r[1] for r in ref]))
     assert sum(counts) == xa.shape[0] and xa.shape[0] > 0
+
+
+def _sub_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # ranks 1 and 2 of a 3-rank world form the group; group ranks 0, 1
+        sub = dist.new_group([1, 2])
+        if rank in (1, 2):
+            n = 3 + rank
+            xyz = torch.full((n, 3), float(rank), dtype=torch.float64)
+            bgr = torch.full((n, 3), rank, dtype=torch.uint8)
+            xa, ca, counts = parallel.gather_cloud(xyz, bgr, dst=0, group=sub)
+            if rank == 1:  # group rank 0 = global rank 1
+                q.put((xa.numpy(), ca.numpy(), counts))
+            else:
+                assert xa is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_cloud_on_a_subgroup():
+    """gather_cloud over a 2-rank subgroup of a 3-rank world: group ranks are
+    mapped to global peers (dst = group rank 0 = global rank 1)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sub_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    xa, ca, counts = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert counts == [4, 5]
+    np.testing.assert_array_equal(xa[:, 0], [1.0] * 4 + [2.0] * 5)
+    np.testing.assert_array_equal(ca[:, 0], [1] * 4 + [2] * 5)
