@@ -74,6 +74,9 @@ def parse(argv=None):
                     help="fast: SL_XYZ_F32_FAST (f32 arithmetic, rel err <= 1.02e-5 of the reference's f64); "
                          "exact: SL_XYZ_F32 (correctly rounded float32 of the reference's f64)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
+    ap.add_argument("--cpu-procs", type=int, default=None,
+                    help="processes of the multi-process CPU leg (default: the core share, multi-view "
+                         "configs only; 0: off)")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per k_decode launch (from profiles/)")
     return ap.parse_args(argv)
@@ -181,6 +184,77 @@ def cpu_baseline(stack_h, tex_h, calib, budget_s):
     return n * px / el, n, el
 
 
+_MP_VIEW = {}
+
+
+def _mp_worker(args):
+    """One process of the P-process CPU baseline: the oracle on the shared view
+    until the deadline; -> views done."""
+    deadline, = args
+    from oracle import sl_oracle
+    st, tx, calib = _MP_VIEW["st"], _MP_VIEW["tx"], _MP_VIEW["calib"]
+    imgs = list(st)
+    n = 0
+    while time.time() < deadline or n == 0:
+        sl_oracle.decode_triangulate(imgs, tx, calib)
+        n += 1
+    return n
+
+
+def cpu_baseline_procs(stack_h, tex_h, calib, procs, budget_s):
+    """The reference's parallelism for many views: one view
+    per process, P processes (fork, before this process touches the GPU), each
+    running the oracle until a common deadline -> (px/s, views, seconds)."""
+    import multiprocessing as mp
+    _MP_VIEW.update(st=stack_h, tx=tex_h, calib=calib)
+    px = stack_h.shape[1] * stack_h.shape[2]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(procs) as pool:
+        t0 = time.time()
+        counts = pool.map(_mp_worker, [(t0 + budget_s,)] * procs)
+        el = time.time() - t0
+    _MP_VIEW.clear()
+    return sum(counts) * px / el, sum(counts), el
+
+
+def host_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    share = os.environ.get("OMP_NUM_THREADS")
+    return {"cpu_model": model, "host_cores": os.cpu_count(),
+            "core_share": int(share) if share and share.isdigit() else None}
+
+
+def cpu_baselines(a, cfg, cfg_idx, gv, calib, rig):
+    """Rank 0, N = 1, before the GPU is touched: the oracle (a NumPy
+    restatement of the reference path, bit-exact to the fixtures the
+    reference produced; oracle/sl_oracle.py) timed on this host: 1 process,
+    and P processes for the multi-view configs (P = the box's core share)."""
+    st, tx = synth.render_stack(rig, seed=1000 * cfg_idx + gv, include_rows=cfg["rows"],
+                                view_deg=cfg["deg"] * gv, device="cpu")
+    st, tx = st.numpy(), tx.numpy()
+    H, W = st.shape[1:]
+    info = host_info()
+    v1, n1, el1 = cpu_baseline(st, tx, calib, a.cpu_seconds)
+    out = {"value": v1, "unit": "px/s", "cores": 1, "kind": "port",
+           "sample": f"{n1} x {W}x{H} view(s), {st.shape[0]} planes, oracle/sl_oracle.py "
+                     f"(NumPy restatement, bit-exact to reference fixtures), 1 process, {el1:.1f} s",
+           **info}
+    procs = a.cpu_procs if a.cpu_procs else (info["core_share"] or min(os.cpu_count() or 1, 16))
+    if a.cpu_procs != 0 and procs > 1 and (cfg["views"] > 1 or a.cpu_procs):
+        vp, np_, elp = cpu_baseline_procs(st, tx, calib, procs, a.cpu_seconds)
+        out["multi_process"] = {"value": vp, "unit": "px/s", "cores": procs, "kind": "port",
+                                "sample": f"{np_} x {W}x{H} view(s) over {procs} processes (one view per "
+                                          f"process at a time), {elp:.1f} s"}
+    return out
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -194,6 +268,11 @@ def main():
         return selftest(a)
     if a.backend != "nccl":
         sys.exit("bench.py: --backend gloo is only for --selftest (the GPU bench gathers over RCCL)")
+    cpu = None
+    if a.cpu_baseline and world == 1 and rank == 0:  # before this process touches the GPU (fork pool)
+        c0 = CONFIGS[a.config]
+        rig0 = synth.Rig(H=c0["H"], W=c0["W"], Wp=c0["Wp"], Hp=c0["Hp"])
+        cpu = cpu_baselines(a, c0, int(a.config[1:]), 0, synth.make_calibration(rig0, with_Nc=False), rig0)
     if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -279,10 +358,9 @@ def main():
     # events' own cost amortised; the per-step events above include it).  Its
     # stack is larger than the 256 MB Infinity Cache, so the re-runs stream
     # from HBM like the steps (rocprofv3's per-dispatch average agrees)
+    _, n_groups, last_px = eng.last_launch_info()  # the launch group time_kernels re-runs
+    v_last = last_px // (H * W)                 # views in the timed (last) group
     t_dec, t_cnt, t_cld = eng.time_kernels(max(a.steps, 10))
-    cpv = -(-H * W // 1024)
-    vpg = max(1, 16384 // cpv)                  # views per launch group (kMaxChunks)
-    v_last = V - vpg * ((V - 1) // vpg)         # views in the timed (last) group
 
     # secondary (maps configs): cloud-only mode (what generate_cloud runs: row planes unread)
     el_cloud = None
@@ -350,14 +428,6 @@ def main():
                     traffic = tj.get("bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
-        cpu = None
-        if a.cpu_baseline and world == 1:
-            one_view = stack[0].cpu().numpy()
-            one_tex = tex[0].cpu().numpy()
-            v_cpu, n_cpu, el_cpu = cpu_baseline(one_view, one_tex, calib, a.cpu_seconds)
-            cpu = {"value": v_cpu, "unit": "px/s", "cores": 1, "kind": "port",
-                   "sample": f"{n_cpu} x {W}x{H} view(s), {n_planes} planes, oracle/sl_oracle.py "
-                             f"(NumPy restatement, bit-exact to reference fixtures), 1 thread, {el_cpu:.1f} s"}
         res = {
             "metric": "decoded+triangulated px/s",
             "value": value,

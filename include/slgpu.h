@@ -149,6 +149,11 @@ int sl_profile_enable(sl_ctx* ctx, int max_calls);
  * recorded calls since the last read, and their count; restarts recording. */
 int sl_profile_read(sl_ctx* ctx, double* decode_ms, double* count_ms, double* cloud_ms, int* calls);
 
+/* The last call's kernel path (0: k_decode + k_count + k_cloud), its number of
+ * launch groups, and the pixels of its last launch group (what
+ * sl_time_kernels re-runs).  Host only. */
+int sl_last_launch_info(sl_ctx* ctx, int* path, int64_t* launches, int64_t* last_launch_px);
+
 /* Blocking, measurement only: re-launches the kernels of the last launch group
  * of the previous sl_decode_triangulate / sl_triangulate_maps call `reps`
  * times each, back to back on its stream, and returns each kernel's average

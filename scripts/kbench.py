@@ -3,8 +3,9 @@ kernel of every call), one process, on a synthetic view (default 4K).
 
     python scripts/kbench.py [--H 2160 --W 3840] [--reps 20] [--only maps+cloud]
 Prints one JSON line per output mode (maps+cloud, cloud, maps, fixed mask):
-kernel microseconds and algorithmic GB/s.  SLGPU_DEBUG selects the
-measurement-only ablations of Params::dbg; SLGPU_LIB a build variant.
+kernel microseconds and algorithmic GB/s, the host cost of a call and the
+wall time per call.  SLGPU_LIB selects a build variant (scripts/build_variants.sh:
+-DSLGPU_ABLATE=... measurement-only ablations and tuning macros).
 """
 import argparse
 import json
@@ -23,6 +24,7 @@ ap.add_argument("--W", type=int, default=3840)
 ap.add_argument("--views", type=int, default=1)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--only", default=None, help="run one variant")
+ap.add_argument("--fast", action="store_true", help="SL_XYZ_F32_FAST clouds")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 rig = synth.Rig(H=a.H, W=a.W)
@@ -52,18 +54,32 @@ for name, kw in [("maps+cloud", dict(maps=True, cloud=True)), ("cloud", dict(map
     if a.only and name != a.only:
         continue
     out = {}
+    if a.fast and kw.get("cloud"):
+        kw = dict(kw, fast_f32=True)
     for _ in range(3):
         eng.decode_triangulate(st, texture=tx, out=out, **kw)
     eng.sync()
     eng.profile_enable(a.reps)
     for _ in range(a.reps):
         eng.decode_triangulate(st, texture=tx, out=out, **kw)
-    d_ms, s_ms, c_ms, n = eng.profile_read()  # decode, count, cloud
+    d_ms, s_ms, c_ms, n = eng.profile_read()  # decode, count, cloud (single pass: fused, stats, 0)
     eng.sync()
+    # host cost of one call (enqueue only, no events)
+    t0 = time.perf_counter()
+    for _ in range(a.reps):
+        eng.decode_triangulate(st, texture=tx, out=out, **kw)
+    host_us = 1e6 * (time.perf_counter() - t0) / a.reps
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(a.reps):
+        eng.decode_triangulate(st, texture=tx, out=out, **kw)
+    eng.sync()
+    wall_us = 1e6 * (time.perf_counter() - t0) / a.reps
     npts = int(out["view_offsets"][-1].item()) if "view_offsets" in out else 0
     planes = st.shape[1] if kw.get("maps") else 2 + 2 * 11
     b = px * planes + (3 * px + 15 * npts if kw.get("cloud") else 0) + (9 * px if kw.get("maps") else 0)
     tot = (s_ms + d_ms + c_ms) / n
-    print(json.dumps({"variant": name, "dbg": os.environ.get("SLGPU_DEBUG", "0"), "count_us": 1e3 * s_ms / n,
+    print(json.dumps({"variant": name, "count_us": 1e3 * s_ms / n,
                       "decode_us": 1e3 * d_ms / n, "cloud_us": 1e3 * c_ms / n, "total_us": 1e3 * tot,
-                      "alg_GBps_total": b / tot / 1e6, "points": npts}))
+                      "alg_GBps_total": b / tot / 1e6, "points": npts, "host_us_per_call": host_us,
+                      "wall_us_per_call": wall_us, "lib": os.path.basename(os.environ.get("SLGPU_LIB", "libslgpu.so"))}))

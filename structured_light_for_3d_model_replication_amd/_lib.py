@@ -32,7 +32,7 @@ SL_XYZ_F32_FAST = 2
 # every symbol include/slgpu.h declares
 EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_error", "sl_ctx_reserve",
            "sl_set_calib", "sl_decode_triangulate", "sl_triangulate_maps", "sl_sync",
-           "sl_last_thresholds", "sl_profile_enable", "sl_profile_read", "sl_time_kernels", "sl_format_ply", "sl_write_ply",
+           "sl_last_thresholds", "sl_last_launch_info", "sl_profile_enable", "sl_profile_read", "sl_time_kernels", "sl_format_ply", "sl_write_ply",
            "sl_write_ply_binary", "sl_voxel_downsample", "sl_statistical_outliers", "sl_select_by_index",
            "sl_transform_points", "sl_merge_pool_trim", "sl_calib_products", "sl_gather_unique_id", "sl_gather_init", "sl_gather_counts",
            "sl_gather",
@@ -55,6 +55,7 @@ _SIGS = {
     "sl_sync": (_i32, [_vp, _vp]),
     "sl_last_thresholds": (_i32, [_vp, _i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                   ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    "sl_last_launch_info": (_i32, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "sl_profile_enable": (_i32, [_vp, _i32]),
     "sl_profile_read": (_i32, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32)]),

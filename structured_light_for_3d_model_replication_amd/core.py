@@ -351,6 +351,16 @@ class Reconstructor:
                                                ctypes.byref(c)), self._ctx, "sl_time_kernels")
         return a.value, b.value, c.value
 
+    def last_launch_info(self):
+        """-> (kernel path, launch groups, pixels of the last launch group) of
+        the last call (sl_last_launch_info); the last group is what
+        ``time_kernels`` re-runs."""
+        path, n, px = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64()
+        with self._lock:
+            _lib.check(self._L.sl_last_launch_info(self._ctx, ctypes.byref(path), ctypes.byref(n),
+                                                   ctypes.byref(px)), self._ctx, "sl_last_launch_info")
+        return path.value, n.value, px.value
+
     def last_thresholds(self, view: int = 0):
         nf, dr = ctypes.c_float(), ctypes.c_float()
         tw, tc = ctypes.c_int(), ctypes.c_int()

@@ -1336,6 +1336,12 @@ struct sl_ctx {
   int nranks = 0, rank = 0;
   int64_t* d_gcounts = nullptr;
   int64_t cap_gcounts = 0;
+  // the last call's stream: a call on another stream first waits for the work
+  // queued there (the scratch above is per context)
+  hipStream_t last_stream = nullptr;
+  hipEvent_t done_ev = nullptr;
+  bool done_valid = false;
+  int64_t last_launches = 0, last_launch_px = 0;  // sl_last_launch_info
   struct {
     bool valid = false;
     Params p[3];
@@ -1504,6 +1510,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     hipEvent_t* gev = (ev && g < kProfGroups) ? ev + 4 * g : nullptr;
     if (gev) HIP_TRY(c, hipEventRecord(gev[0], s));
     const int nv = std::min(vpg, p0.n_views - v0);
+    c->last_launch_px = static_cast<int64_t>(nv) * p0.HW;
     Params p = p0;
     p.n_views = nv;
     p.n_chunks = static_cast<int64_t>(nv) * cpv;
@@ -1569,6 +1576,20 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     if (gev) HIP_TRY(c, hipEventRecord(gev[3], s));
   }
   if (ev) c->prof_groups.push_back(std::min(g, kProfGroups));
+  c->last_launches = g;
+  return SL_OK;
+}
+
+// The context's scratch is shared by its calls: a call on another stream than
+// the previous call's first waits for the work queued on that stream (an event
+// recorded there now), so calls on one context never overlap on the device.
+int stream_handoff(sl_ctx* c, hipStream_t s) {
+  if (c->done_valid && s != c->last_stream) {
+    HIP_TRY(c, hipEventRecord(c->done_ev, c->last_stream));
+    HIP_TRY(c, hipStreamWaitEvent(s, c->done_ev, 0));
+  }
+  c->last_stream = s;
+  c->done_valid = true;
   return SL_OK;
 }
 
@@ -1710,6 +1731,10 @@ int sl_ctx_create(int device, sl_ctx** out) {
   if (const char* d = getenv("SLGPU_DECODE_PER_CU")) per_cu = atoi(d);
   if (per_cu > 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
     c->decode_wgs = per_cu * n_cu;
+  if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
+    delete c;
+    return SL_EHIP;
+  }
   *out = c;
   return SL_OK;
 }
@@ -1721,6 +1746,7 @@ void sl_ctx_destroy(sl_ctx* c) {
     if (Rccl* R = rccl()) (void)R->comm_destroy(static_cast<ncclComm_t>(c->comm));
   }
   if (c->d_gcounts) (void)hipFree(c->d_gcounts);
+  if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (void* ptr : {static_cast<void*>(c->d_planes), static_cast<void*>(c->d_xn), static_cast<void*>(c->d_yn),
                     static_cast<void*>(c->d_nc), static_cast<void*>(c->d_stats), static_cast<void*>(c->d_f32),
@@ -1928,7 +1954,10 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
                    (!tex || (aligned16(tex) && tex_vs % 16 == 0)) &&
                    (!maps || (aligned16(col_out) && aligned16(row_out) && aligned16(mask_out)));
   HIP_TRY(c, hipSetDevice(c->device));
-  return launch(c, p, vec, decode_mode, count_mode, cloud_mode, static_cast<hipStream_t>(stream));
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  r = stream_handoff(c, s);
+  if (r) return r;
+  return launch(c, p, vec, decode_mode, count_mode, cloud_mode, s);
 }
 
 int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, const uint8_t* tex,
@@ -1956,7 +1985,10 @@ int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, 
   const int cloud_mode = xyz_mode_bits(c, xyz_dtype, poses);
   const bool vec = (W % 16 == 0) && W >= 64 && aligned16(col_map) && aligned16(mask) && aligned16(tex);
   HIP_TRY(c, hipSetDevice(c->device));
-  return launch(c, p, vec, decode_mode, count_mode, cloud_mode, static_cast<hipStream_t>(stream));
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  r = stream_handoff(c, s);
+  if (r) return r;
+  return launch(c, p, vec, decode_mode, count_mode, cloud_mode, s);
 }
 
 int sl_sync(sl_ctx* c, void* stream) {
@@ -2051,6 +2083,14 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
   if (count_ms) *count_ms = out[1];
   if (cloud_ms) *cloud_ms = out[2];
   return r;
+}
+
+int sl_last_launch_info(sl_ctx* c, int* path, int64_t* launches, int64_t* last_launch_px) {
+  if (!c) return SL_EINVAL;
+  if (path) *path = 0;
+  if (launches) *launches = c->last_launches;
+  if (last_launch_px) *last_launch_px = c->last_launch_px;
+  return SL_OK;
 }
 
 int sl_last_thresholds(sl_ctx* c, int view, float* nf, float* dr, int* thr_w, int* thr_c) {
