@@ -114,6 +114,8 @@ constexpr int M_NC = 16;       // rays from a device Nc table instead of pinhole
 constexpr int M_ROWS = 32;     // k_decode: decode the row sequence
 constexpr int M_HIST = 64;     // adaptive mask: k_decode builds the histogram, k_count reads it
 constexpr int M_FAST32 = 128;  // k_cloud: f32 arithmetic for well-conditioned points (SL_XYZ_F32_FAST)
+constexpr int M_DECIDE = 256;  // k_decode: also the mask and the |n.r| decision (k_count's work; k_stats
+                               // histograms): mask map, point nibbles, chunk counts, block sums
 constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
 
 constexpr int kSlot = 272;                 // histogram of one view: 256 bins + max + pad (u32)
@@ -147,7 +149,7 @@ static_assert(sizeof(ViewStats) % 64 == 0, "ViewStats keeps 64-B alignment");
 struct Params {
   const uint8_t* stack;
   int64_t stack_vs;
-  int view_bytes;  // n_img * H * W (< 2^31): buffer-descriptor range of one view's stack
+  int view_bytes;  // min(n_img * H * W, 2^31 - 1) (informational; k_decode uses a descriptor per plane)
   const uint8_t* tex;
   int64_t tex_vs;
   const int32_t* in_col;
@@ -359,6 +361,106 @@ __device__ __forceinline__ bool has_point(const Params& p, int mode, const float
   return has_point_f64(p.planes, p.xn, p.yn, (mode & M_NC) ? p.nc_rays : nullptr, p.HW, c, u, v, q);
 }
 
+
+// ------------------------------------------------------------------ k_stats ----
+// The adaptive mask's two global reductions (sl_system.py:526-528) ahead of a
+// launch group whose k_decode applies the mask itself (M_DECIDE): per view,
+// the black-plane 256-bin histogram and max(white - black), per workgroup in
+// LDS (bank-skewed replicas, as k_decode's), flushed into kHistRepl replicas
+// of the view's histogram (block % kHistRepl: the flush atomics of all
+// workgroups spread over 8 rows instead of one).
+constexpr int kHistRepl = 8;
+constexpr int kHistView = kHistRepl * kSlot;  // u32 per view
+
+// grid (blocks per view, views of the group); 16 pixels per thread per step.
+__global__ __launch_bounds__(kThreads) void k_stats(Params p) {
+  __shared__ unsigned s_hist[256 * kHistStride];
+  __shared__ int s_max[kWaves];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int view = blockIdx.y;
+  const int64_t HW = p.HW;
+  if (blockIdx.x == 0)  // the next launch group's histograms of this slot (its scratch here)
+    for (int i = tid; i < kHistView; i += kThreads) p.hist_zero[static_cast<int64_t>(view) * kHistView + i] = 0u;
+  for (int i = tid; i < 256 * kHistStride; i += kThreads) s_hist[i] = 0u;
+  __syncthreads();
+  const uint8_t* vb = p.stack + view * p.stack_vs;
+  unsigned* hrow = s_hist + (lane & (kHistRep - 1));
+  int mx = -1024;
+  const int64_t n16 = HW / 16;  // HW % 16 == 0 on this path
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + tid; i < n16;
+       i += static_cast<int64_t>(gridDim.x) * kThreads) {
+    const uint4 wq = *reinterpret_cast<const uint4*>(vb + 16 * i);
+    const uint4 bq = *reinterpret_cast<const uint4*>(vb + HW + 16 * i);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int bk = static_cast<int>(byte_of(bq, k));
+      atomicAdd(hrow + bk * kHistStride, 1u);
+      mx = max(mx, static_cast<int>(byte_of(wq, k)) - bk);
+    }
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
+  if (lane == 0) s_max[wid] = mx;
+  __syncthreads();
+  unsigned* gh = p.hist + static_cast<int64_t>(view) * kHistView + (blockIdx.x % kHistRepl) * kSlot;
+  unsigned cnt = 0u;
+  const unsigned* row = s_hist + tid * kHistStride;
+#pragma unroll
+  for (int r = 0; r < kHistRep; ++r) cnt += row[r];
+  if (cnt) atomicAdd(gh + tid, cnt);
+  if (tid == 0) {
+    int m = s_max[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) m = max(m, s_max[w]);
+    if (m > -1024) atomicMax(gh + 256, static_cast<unsigned>(m + 1024));
+  }
+}
+
+// Thresholds of a view from its kHistRepl histogram replicas (one wave).
+__device__ __forceinline__ Thresholds view_thresholds(const Params& p, int view, int lane) {
+  uint4 b4 = make_uint4(0u, 0u, 0u, 0u);
+  unsigned hmax = 0u;
+  const unsigned* h = p.hist + static_cast<int64_t>(view) * kHistView;
+#pragma unroll
+  for (int r = 0; r < kHistRepl; ++r) {
+    const uint4 t = reinterpret_cast<const uint4*>(h + r * kSlot)[lane];
+    b4.x += t.x;
+    b4.y += t.y;
+    b4.z += t.z;
+    b4.w += t.w;
+    hmax = max(hmax, h[r * kSlot + 256]);
+  }
+  return thresholds_from_bins(b4, hmax, p.HW, lane);
+}
+
+// Mask of 4 packed pixels (one word of white / black bytes): bit e = pixel e
+// has white > tw and white - black > tc (sl_system.py:534-535); byte-SWAR in
+// 16-bit lanes as k_count (tw2 = (tw + 1) * 0x10001, tc2 = (tc + 17) * 0x10001;
+// exact for 0 <= tw + 1 <= 0x7000, -17 <= tc <= 0x7000: adaptive thresholds
+// are in [0, 382] x [-13, 12], fixed ones 40 / 10).  *bytes: the 0/1 mask bytes.
+__device__ __forceinline__ uint32_t mask4(uint32_t w, uint32_t b, uint32_t tw2, uint32_t tc2, uint32_t* bytes) {
+  const uint32_t we = w & 0x00ff00ffu, wo = (w >> 8) & 0x00ff00ffu;
+  const uint32_t be = b & 0x00ff00ffu, bo = (b >> 8) & 0x00ff00ffu;
+  const uint32_t me = ((we | 0x80008000u) - tw2) & (((we + 0x00100010u) | 0x80008000u) - (be + tc2));
+  const uint32_t mo = ((wo | 0x80008000u) - tw2) & (((wo + 0x00100010u) | 0x80008000u) - (bo + tc2));
+  const uint32_t y = ((me >> 15) & 0x00010001u) | ((mo >> 7) & 0x01000100u);
+  *bytes = y;
+  return (y & 1u) | ((y >> 7) & 2u) | ((y >> 14) & 4u) | ((y >> 21) & 8u);
+}
+
+// k_decode M_DECIDE: the f32 plane table, xn = (u - cx) / fx and yn =
+// (v - cy) / fy in LDS (host: Wp <= kDecPl, W <= kDecX, H <= kDecY; the
+// launch's grid is capped at a few workgroups per CU, so the fill is cheap).
+#ifndef SLGPU_DEC_YN_LDS
+#define SLGPU_DEC_YN_LDS 0
+#endif
+constexpr bool kDecYnLds = SLGPU_DEC_YN_LDS != 0;  // yn in LDS (else one early global load per lane)
+constexpr int kDecPl = 2048, kDecX = 4096, kDecY = 4096;
+constexpr int kDecodeLds = (kDecPl * 4 + kDecX + (kDecYnLds ? kDecY : 0)) * 4;  // bytes: > the histogram replicas
+static_assert(kDecodeLds >= 256 * kHistStride * 4, "the decode LDS holds the histogram replicas too");
+
 // ================================================================ k_decode ====
 // gray_decode (sl_system.py:519-577) for one chunk per wave, in the streaming
 // layout (lane l owns the chunk's pixels [16 l, 16 l + 16)): column and row
@@ -375,11 +477,11 @@ __device__ __forceinline__ bool has_point(const Params& p, int mode, const float
 // Grid (chunk groups, views); waves past the view's last chunk run empty (the
 // workgroup barriers count them).
 #ifndef SLGPU_DECODE_PER_CU
-#define SLGPU_DECODE_PER_CU 2
+#define SLGPU_DECODE_PER_CU 3
 #endif
 constexpr int kDecodePerCu = SLGPU_DECODE_PER_CU;  // default k_decode grid cap, workgroups per CU (0: none)
 #ifndef SLGPU_DECODE_WAVES
-#define SLGPU_DECODE_WAVES 1
+#define SLGPU_DECODE_WAVES 3
 #endif
 template <int KC, int KR, int MODE, int VEC>
 __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params p) {
@@ -388,15 +490,33 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   const int krr = (mode & M_ROWS) ? (KR >= 0 ? KR : p.kr) : 0;
   const int nc = p.nc, nr = p.nr;
   const bool vec = VEC > 0;
-  const bool hist = (mode & M_HIST) != 0;
+  const bool hist = (mode & M_HIST) && !(mode & M_DECIDE);  // accumulate the histogram (else: k_stats did)
 
-  __shared__ unsigned s_hist[256 * kHistStride];
+  // LDS: the histogram replicas (M_HIST), or the decision's tables (M_DECIDE)
+  __shared__ __attribute__((aligned(16))) unsigned s_lds[kDecodeLds / 4];
   __shared__ int s_max[kWaves];
+  __shared__ int s_cnt[2][kWaves];
+  unsigned* s_hist = s_lds;
+  float4* s_pl = reinterpret_cast<float4*>(s_lds);
+  float* s_xn = reinterpret_cast<float*>(s_lds) + 4 * kDecPl;
+  float* s_yn = s_xn + kDecX;
+  const bool decide = (mode & M_DECIDE) != 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
   const int64_t HW = p.HW;
+  if (decide) {
+    for (int i = tid; i < p.Wp; i += kThreads) s_pl[i] = p.planes32[i];
+    for (int i = tid; i < p.W; i += kThreads) s_xn[i] = p.xn32[i];
+    if (kDecYnLds)
+      for (int i = tid; i < p.H; i += kThreads) s_yn[i] = p.yn32[i];
+    __syncthreads();
+  }
+  int cur_view = -1;                                               // M_DECIDE: the wave's thresholds
+  uint32_t tw2 = static_cast<uint32_t>(40 + 1) * 0x00010001u;      // fixed mask:
+  uint32_t tc2 = static_cast<uint32_t>(10 + 17) * 0x00010001u;     // multi_point_cloud_process.py:36-38
+  int it = 0;
 
   // the next launch's histogram (scratch of this one)
   if (hist && blockIdx.x == 0)
@@ -419,6 +539,10 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   const int64_t pxl = n_px > 0 ? px0 : 0;  // keep loads unconditional and in bounds
   const int64_t o = view * HW + px0;
 
+  // M_DECIDE without yn in LDS: the row's yn first (the oldest load: waiting
+  // for it never waits for this iteration's stores)
+  const float ys_early = (decide && !kDecYnLds && (mode & M_CODES) && n_px > 0)
+                             ? p.yn32[static_cast<int>(px0) / p.W] : 0.0f;
   uint32_t col[kPx];
   if (mode & M_FROMMAPS) {
     // reconstruct_point_cloud's input col_map (clipped below, sl_system.py:626)
@@ -441,12 +565,13 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
     // Plane loads: on the vector path a buffer descriptor of the view's stack
     // (SGPRs) + the lane's 32-bit pixel offset + the plane offset in an SGPR.
     const uint8_t* vbase = p.stack + view * p.stack_vs;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vbase), 0, p.view_bytes, 0x00020000);
     const int voff = static_cast<int>(pxl);
     auto ldp = [&](int plane) -> uint4 {
       if (vec) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, plane * static_cast<int>(HW), kLoadAux);
+        // a descriptor per plane (SGPRs): one plane, not the view's stack, must be < 2 GiB
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(vbase) + static_cast<int64_t>(plane) * HW, 0, static_cast<int>(HW), 0x00020000);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, kLoadAux);
         return make_uint4(v[0], v[1], v[2], v[3]);
       }
       return ld16(vbase + pxl + static_cast<int64_t>(plane) * HW, n_px, false);
@@ -555,6 +680,89 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         }
       }
     }
+    if (decide) {
+      // ---- mask with the view's thresholds (wave-cached; k_stats' histograms) ----
+      if ((mode & M_HIST) && view != cur_view) {
+        const Thresholds t = view_thresholds(p, view, lane);
+        tw2 = static_cast<uint32_t>(t.white + 1) * 0x00010001u;
+        tc2 = static_cast<uint32_t>(t.contrast + 17) * 0x00010001u;
+        if (civ == 0 && lane == 0) {
+          p.stats[view].thr_white = t.white;
+          p.stats[view].thr_contrast = t.contrast;
+          p.stats[view].noise_floor = t.noise_floor;
+          p.stats[view].dynamic_range = t.dynamic_range;
+        }
+        cur_view = view;
+      }
+      uint32_t ok = 0u, mb[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) ok |= mask4(word(wq, w), word(bq, w), tw2, tc2, &mb[w]) << (4 * w);
+      if (n_px != kPx) ok = 0u;  // vec: whole 16-pixel groups
+      if ((mode & M_MAPS) && n_px == kPx)
+        *reinterpret_cast<uint4*>(p.mask_out + o) = make_uint4(mb[0], mb[1], mb[2], mb[3]);
+      // ---- |n.r| > 1e-6 (sl_system.py:638-642) of the masked pixels, LDS tables ----
+      uint32_t pt = 0u;
+      if ((mode & M_CODES) && ok) {
+        const int px0i = static_cast<int>(px0);
+        const int v = px0i / p.W, u0 = px0i - v * p.W;  // the lane's 16 pixels share row v (W % 16 == 0)
+        float4 pf[kPx];
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) pf[k] = s_pl[min(col[k], static_cast<uint32_t>(p.Wp - 1))];
+        float xs[kPx];
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const float4 x4 = reinterpret_cast<const float4*>(s_xn + u0)[q4];
+          xs[4 * q4] = x4.x;
+          xs[4 * q4 + 1] = x4.y;
+          xs[4 * q4 + 2] = x4.z;
+          xs[4 * q4 + 3] = x4.w;
+        }
+        const float ys = kDecYnLds ? s_yn[v] : ys_early;
+        uint32_t todo = ok;
+        if (!(mode & M_NC)) {  // k_count's one-compare sufficient test (p.fast_thr, sl_set_calib)
+#pragma unroll
+          for (int k = 0; k < kPx; ++k) {
+            const float a = fabsf(__builtin_fmaf(pf[k].x, xs[k], __builtin_fmaf(pf[k].y, ys, pf[k].z)));
+            if (a > p.fast_thr) pt |= 1u << k;
+          }
+          pt &= ok;
+          todo &= ~pt;
+        }
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) {  // the bounded f32 test, f64 where undecided
+          if (!((todo >> k) & 1u)) continue;
+          const int c = static_cast<int>(min(col[k], static_cast<uint32_t>(p.Wp - 1)));
+          const int64_t q = px0 + k;
+          float x, y, z, inv;
+          if (mode & M_NC) {
+            x = static_cast<float>(p.nc_rays[q]);
+            y = static_cast<float>(p.nc_rays[HW + q]);
+            z = static_cast<float>(p.nc_rays[2 * HW + q]);
+            inv = 1.0f;
+          } else {
+            x = xs[k];
+            y = ys;
+            z = 1.0f;
+            inv = __frsqrt_rn(x * x + y * y + 1.0f);
+          }
+          if (has_point(p, mode, pf[k], c, x, y, z, inv, u0 + k, v, q)) pt |= 1u << k;
+        }
+      }
+      if (mode & M_CODES) {
+        // point nibbles in k_count's layout (byte 64 s + l: pixels 256 s + 4 l + e):
+        // this lane's 16 pixels are the 4 bytes at 4 lane
+        const int64_t gci = static_cast<int64_t>(view) * p.cpv + civ;
+        if (live) {
+          const uint32_t nw = (pt & 0xfu) | ((pt & 0xf0u) << 4) | ((pt & 0xf00u) << 8) | ((pt & 0xf000u) << 12);
+          *reinterpret_cast<uint32_t*>(p.ptnib + gci * kChunkNib + 4 * lane) = nw;
+        }
+        const int cnt = wave_sum(__popc(pt));
+        if (lane == 0) {
+          if (live) p.chunk_counts[gci] = cnt;
+          s_cnt[it & 1][wid] = live ? cnt : 0;
+        }
+      }
+    }
     if (hist) {
       unsigned* hrow = s_hist + (lane & (kHistRep - 1));
       int mx = -1024;
@@ -589,6 +797,16 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         if (k < n_px) p.codes[o + k] = static_cast<uint16_t>(rec[k >> 1] >> (16 * (k & 1)));
     }
   }
+  if (decide && (mode & M_CODES)) {  // the workgroup's block sum (k_count's, for k_cloud's offsets)
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) t += s_cnt[it & 1][w];
+      p.block_sums[static_cast<int64_t>(view) * ngroups + cg] = t;
+    }
+  }
+  ++it;
   }  // chunk groups
 
   if (hist) {
@@ -713,7 +931,9 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
   const bool swar = vec && thr_w >= -1 && thr_w < 0x7000 && thr_c >= -17 && thr_c < 0x7000;
   const uint32_t tw2 = static_cast<uint32_t>(thr_w + 1) * 0x00010001u;
   const uint32_t tc2 = static_cast<uint32_t>(thr_c + 17) * 0x00010001u;
-  uint32_t ok[4];  // bit e: pixel 256 s + 4 lane + e is valid
+  uint32_t ok[4];      // bit e: pixel 256 s + 4 lane + e is valid
+  uint32_t mbytes[4];  // the mask map words (vec), stored after the plane gathers below:
+                       // vmcnt counts stores too, so a gather issued after a store waits for it
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int px = cpx + 256 * s + 4 * lane;
@@ -737,7 +957,8 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
       bytes = (m & 1u) | ((m & 2u) << 7) | ((m & 4u) << 14) | ((m & 8u) << 21);
     }
     ok[s] = m;
-    if (mode & M_MAPS) {
+    mbytes[s] = bytes;
+    if ((mode & M_MAPS) && (!vec || !codes)) {
       uint8_t* mo_ = p.mask_out + static_cast<int64_t>(view) * HW;
       if (vec) {
         if (px < HW) *reinterpret_cast<uint32_t*>(mo_ + px) = bytes;
@@ -755,6 +976,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
   // second pair's gathers out of the first pair's registers: 4 waves / SIMD)
   const int v_c = cpx / W, u_c = cpx - v_c * W;  // chunk origin
   int total = 0;
+  uint32_t nibs[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     if (s == 2) __builtin_amdgcn_sched_barrier(0);
@@ -845,8 +1067,19 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
       }
     }
     total += __popc(nib);
-    // point nibble of (step s, lane): one byte, pixel order within the chunk
-    p.ptnib[gc * kChunkNib + 64 * s + lane] = static_cast<uint8_t>(nib);
+    nibs[s] = nib;
+  }
+  // stores last (after every gather of the wave): the point nibbles of (step
+  // s, lane), one byte each in pixel order within the chunk, and the mask map
+#pragma unroll
+  for (int s = 0; s < 4; ++s) p.ptnib[gc * kChunkNib + 64 * s + lane] = static_cast<uint8_t>(nibs[s]);
+  if ((mode & M_MAPS) && vec) {
+    uint8_t* mo_ = p.mask_out + static_cast<int64_t>(view) * HW;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int px = cpx + 256 * s + 4 * lane;
+      if (px < HW) *reinterpret_cast<uint32_t*>(mo_ + px) = mbytes[s];
+    }
   }
   total = wave_sum(total);
   if (lane == 0) p.chunk_counts[gc] = total;
@@ -1329,6 +1562,9 @@ struct sl_ctx {
   // optional per-call HIP-event timing of k_decode / k_count / k_cloud
   std::vector<hipEvent_t> prof_ev;  // kProfEv events per call slot
   std::vector<int> prof_groups;     // launch groups recorded per call
+  std::vector<char> prof_decide;    // per call: M_DECIDE path (events around k_stats, k_decode, k_cloud)
+  int n_cu = 0;
+  bool force_3k = false;            // SLGPU_PATH=3: k_decode + k_count + k_cloud for aligned frames too (A/B)
   int prof_n = 0;
   // the last launch group's kernels and arguments (sl_time_kernels)
   // RCCL gather (sl_gather_init): communicator, this rank, count scratch
@@ -1344,6 +1580,7 @@ struct sl_ctx {
   int64_t last_launches = 0, last_launch_px = 0;  // sl_last_launch_info
   struct {
     bool valid = false;
+    bool decide = false;  // fn[1] = k_stats (or null) instead of k_count
     Params p[3];
     const void* fn[3] = {nullptr, nullptr, nullptr};  // k_decode, k_count, k_cloud (or null)
     dim3 grid[3];
@@ -1451,7 +1688,7 @@ int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes) {
   if (r) return r;
   for (int b = 0; b < 2; ++b) {
     const int64_t before = c->cap_hist[b];
-    r = grow(c, &c->d_hist[b], &c->cap_hist[b], views * kSlot);
+    r = grow(c, &c->d_hist[b], &c->cap_hist[b], views * kHistView);  // k_stats' replicas (k_decode's: kSlot)
     if (r) return r;
     if (c->cap_hist[b] != before) c->hist_dirty[b] = 0;  // fresh (zeroed) allocation
   }
@@ -1462,6 +1699,7 @@ int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes) {
 using KernelFn = void (*)(Params);
 constexpr int kProfGroups = 64;            // launch groups timed per call (at most)
 constexpr int kProfEv = 4 * kProfGroups;   // events per call: per group before k_decode, k_count, k_cloud, after
+                                           // (M_DECIDE: before k_stats, k_decode, k_cloud, after)
 
 // k_decode specialisations for the benchmark configurations; everything else
 // (other bit counts, unaligned frames) runs the generic instantiation.
@@ -1476,6 +1714,14 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
     if (mode == ch && kc == 10) return k_decode<10, 0, ch, 1>;
     if (mode == mrc && kc == 11 && kr == 11) return k_decode<11, 11, mrc, 1>;
     if (mode == cc && kc == 11) return k_decode<11, 0, cc, 1>;
+    constexpr int D = M_DECIDE;
+    if (mode == (mrch | D) && kc == 11 && kr == 11) return k_decode<11, 11, mrch | D, 1>;
+    if (mode == (mrch | D) && kc == 10 && kr == 0) return k_decode<10, 0, mrch | D, 1>;
+    if (mode == (mrh | D) && kc == 11 && kr == 11) return k_decode<11, 11, mrh | D, 1>;
+    if (mode == (ch | D) && kc == 11) return k_decode<11, 0, ch | D, 1>;
+    if (mode == (ch | D) && kc == 10) return k_decode<10, 0, ch | D, 1>;
+    if (mode == (mrc | D) && kc == 11 && kr == 11) return k_decode<11, 11, mrc | D, 1>;
+    if (mode == (cc | D) && kc == 11) return k_decode<11, 0, cc | D, 1>;
   }
   return vec ? k_decode<-1, -1, -1, 1> : k_decode<-1, -1, -1, 0>;
 }
@@ -1489,11 +1735,14 @@ KernelFn pick_cloud(int mode, bool vec) {
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // Enqueue, per launch group of views, k_decode -> k_count [-> k_cloud] on
-// stream s.  decode_mode / count_mode / cloud_mode (< 0: no cloud) are the
-// kernels' mode bits.  Launch groups hold at most kMaxChunks chunks (at least
-// one view); a group's points follow the earlier groups' (base_in).
+// stream s -- or, when decode_mode has M_DECIDE, [k_stats ->] k_decode
+// [-> k_cloud] (k_decode applies the mask and makes the point decision).
+// decode_mode / count_mode / cloud_mode (< 0: no cloud) are the kernels' mode
+// bits.  Launch groups hold at most kMaxChunks chunks (at least one view); a
+// group's points follow the earlier groups' (base_in).
 int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mode, int cloud_mode,
            hipStream_t s) {
+  const bool decide = (decode_mode & M_DECIDE) != 0;
   const int64_t cpv = p0.cpv;
   const int vpg = static_cast<int>(std::max<int64_t>(1, kMaxChunks / cpv));  // views per group
   const bool adaptive = (decode_mode & M_HIST) != 0;
@@ -1529,14 +1778,15 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     p.ptnib = c->d_ptnib;
     p.chunk_counts = c->d_chunk_counts;
     p.block_sums = c->d_block_sums;
-    if (adaptive) {
+    if (adaptive) {  // hist_dirty: leading words of a buffer that may be non-zero
       const int a = c->par, b = 1 - c->par;
+      const int64_t words = static_cast<int64_t>(nv) * (decide ? kHistView : kSlot);
       if (c->hist_dirty[a] > 0)
-        HIP_TRY(c, hipMemsetAsync(c->d_hist[a], 0, sizeof(unsigned) * kSlot * c->hist_dirty[a], s));
+        HIP_TRY(c, hipMemsetAsync(c->d_hist[a], 0, sizeof(unsigned) * c->hist_dirty[a], s));
       p.hist = c->d_hist[a];
       p.hist_zero = c->d_hist[b];
-      c->hist_dirty[a] = nv;
-      if (c->hist_dirty[b] <= nv) c->hist_dirty[b] = 0;
+      c->hist_dirty[a] = words;  // accumulated now; this launch zeroes b's leading `words`
+      if (c->hist_dirty[b] <= words) c->hist_dirty[b] = 0;
       c->par = b;
     }
     const dim3 grid(static_cast<unsigned>((cpv + kWaves - 1) / kWaves), static_cast<unsigned>(nv));
@@ -1547,6 +1797,22 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     c->last.grid[1] = c->last.grid[2] = grid;
     c->last.s = s;
     c->last.fn[2] = nullptr;
+    c->last.decide = decide;
+    if (decide) {
+      c->last.fn[1] = nullptr;
+      if (adaptive) {  // k_stats: the thresholds' histograms, before the decode applies them
+        const int64_t per_view = (p0.HW / 16 + kThreads - 1) / kThreads;
+        const dim3 sg(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(per_view, (2 * c->n_cu + nv - 1) / nv))),
+                      static_cast<unsigned>(nv));
+        p.mode = decode_mode;
+        void* args[] = {&p};
+        c->last.p[1] = p;
+        c->last.fn[1] = reinterpret_cast<const void*>(k_stats);
+        c->last.grid[1] = sg;
+        HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(k_stats), sg, dim3(kThreads), args, 0, s));
+      }
+      if (gev) HIP_TRY(c, hipEventRecord(gev[1], s));
+    }
     {
       p.mode = decode_mode;
       void* args[] = {&p};
@@ -1555,8 +1821,8 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->last.fn[0] = reinterpret_cast<const void*>(fn);
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dgrid, dim3(kThreads), args, 0, s));
     }
-    if (gev) HIP_TRY(c, hipEventRecord(gev[1], s));
-    {
+    if (gev) HIP_TRY(c, hipEventRecord(gev[decide ? 2 : 1], s));
+    if (!decide) {
       p.mode = count_mode;
       void* args[] = {&p};
       const void* fn = vec ? reinterpret_cast<const void*>(k_count<1>) : reinterpret_cast<const void*>(k_count<0>);
@@ -1564,7 +1830,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->last.fn[1] = fn;
       HIP_TRY(c, hipLaunchKernel(fn, grid, dim3(kThreads), args, 0, s));
     }
-    if (gev) HIP_TRY(c, hipEventRecord(gev[2], s));
+    if (gev && !decide) HIP_TRY(c, hipEventRecord(gev[2], s));
     if (cloud_mode >= 0) {
       p.mode = cloud_mode;
       void* args[] = {&p};
@@ -1575,7 +1841,10 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     }
     if (gev) HIP_TRY(c, hipEventRecord(gev[3], s));
   }
-  if (ev) c->prof_groups.push_back(std::min(g, kProfGroups));
+  if (ev) {
+    c->prof_groups.push_back(std::min(g, kProfGroups));
+    c->prof_decide.push_back(decide);
+  }
   c->last_launches = g;
   return SL_OK;
 }
@@ -1729,8 +1998,11 @@ int sl_ctx_create(int device, sl_ctx** out) {
   // default kDecodePerCu; 0 = uncapped)
   int per_cu = kDecodePerCu, n_cu = 0;
   if (const char* d = getenv("SLGPU_DECODE_PER_CU")) per_cu = atoi(d);
-  if (per_cu > 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess)
-    c->decode_wgs = per_cu * n_cu;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < 1)
+    n_cu = 256;
+  c->n_cu = n_cu;
+  if (per_cu > 0) c->decode_wgs = per_cu * n_cu;
+  if (const char* d = getenv("SLGPU_PATH")) c->force_3k = atoi(d) == 3;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
@@ -1925,13 +2197,14 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
     idx += 2;
     ++pairs;
   }
-  if (static_cast<int64_t>(n_img) * HW >= (1ll << 31) || 3 * HW >= (1ll << 31))
-    return fail(c, SL_EINVAL, "one view's stack must be < 2 GiB");
+  // k_decode reads each plane through a buffer descriptor of its own: a plane
+  // (not a view's stack) must stay under 2 GiB; pixel offsets are 32-bit
+  if (3 * HW >= (1ll << 31)) return fail(c, SL_EINVAL, "a frame must have fewer than 2^31 / 3 pixels");
   Params p;
   fill_common(c, p, n_views, H, W);
   p.stack = stack;
   p.stack_vs = stack_vs;
-  p.view_bytes = static_cast<int>(static_cast<int64_t>(n_img) * HW);
+  p.view_bytes = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(n_img) * HW, INT32_MAX));
   p.tex = tex;
   p.tex_vs = tex_vs;
   p.nc = nc;
@@ -1953,11 +2226,14 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   const bool vec = (W % 16 == 0) && W >= 64 && aligned16(stack) && (stack_vs % 16 == 0) &&
                    (!tex || (aligned16(tex) && tex_vs % 16 == 0)) &&
                    (!maps || (aligned16(col_out) && aligned16(row_out) && aligned16(mask_out)));
+  // aligned frames whose f32 tables fit k_decode's LDS: mask + decision in
+  // k_decode ([k_stats] + k_decode + k_cloud), else k_decode + k_count + k_cloud
+  const bool decide = vec && !c->force_3k && W <= kDecX && H <= kDecY && (!xyz || c->Wp <= kDecPl);
   HIP_TRY(c, hipSetDevice(c->device));
   const hipStream_t s = static_cast<hipStream_t>(stream);
   r = stream_handoff(c, s);
   if (r) return r;
-  return launch(c, p, vec, decode_mode, count_mode, cloud_mode, s);
+  return launch(c, p, vec, decide ? (decode_mode | M_DECIDE) : decode_mode, count_mode, cloud_mode, s);
 }
 
 int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, const uint8_t* tex,
@@ -2005,6 +2281,7 @@ int sl_profile_enable(sl_ctx* c, int max_calls) {
   for (hipEvent_t e : c->prof_ev) HIP_TRY(c, hipEventDestroy(e));
   c->prof_ev.clear();
   c->prof_groups.clear();
+  c->prof_decide.clear();
   c->prof_n = 0;
   for (int i = 0; i < kProfEv * max_calls; ++i) {
     hipEvent_t e;
@@ -2023,14 +2300,16 @@ int sl_profile_read(sl_ctx* c, double* decode_ms, double* count_ms, double* clou
     for (int g = 0; g < ng; ++g) {
       hipEvent_t* ev = &c->prof_ev[kProfEv * i + 4 * g];
       HIP_TRY(c, hipEventSynchronize(ev[3]));
+      const bool dz = i < static_cast<int>(c->prof_decide.size()) && c->prof_decide[i];
       for (int k = 0; k < 3; ++k) {
         float ms = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
-        t[k] += ms;
+        t[dz ? (k == 0 ? 1 : k == 1 ? 0 : 2) : k] += ms;  // M_DECIDE: (k_stats, k_decode, k_cloud)
       }
     }
   }
   c->prof_groups.clear();
+  c->prof_decide.clear();
   if (decode_ms) *decode_ms = t[0];
   if (count_ms) *count_ms = t[1];
   if (cloud_ms) *cloud_ms = t[2];
@@ -2050,7 +2329,10 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
   // k_count and k_cloud first: they read k_decode's records and histogram,
   // which k_decode's re-runs then overwrite (records identically; the
   // histograms accumulate and are reset below)
-  const int order[3] = {1, 2, 0};
+  // (M_DECIDE: k_cloud, then k_decode -- it reads the histograms k_stats'
+  // re-runs accumulate into -- then k_stats)
+  const int order3[3] = {1, 2, 0}, orderd[3] = {2, 0, 1};
+  const int* order = c->last.decide ? orderd : order3;
   HIP_TRY(c, hipEventRecord(ev[0], s));
   for (int q = 0; q < 3 && r == SL_OK; ++q) {
     const int k = order[q];
@@ -2077,7 +2359,7 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
   }
   for (int k = 0; k < 4; ++k) (void)hipEventDestroy(ev[k]);
   // the re-runs accumulated into the histograms: the next calls start from zero
-  for (int b = 0; b < 2; ++b) c->hist_dirty[b] = c->cap_hist[b] / kSlot;
+  for (int b = 0; b < 2; ++b) c->hist_dirty[b] = c->cap_hist[b];
   c->last.valid = false;
   if (decode_ms) *decode_ms = out[0];
   if (count_ms) *count_ms = out[1];
