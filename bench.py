@@ -77,8 +77,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-procs", type=int, default=None,
                     help="processes of the multi-process CPU leg (default: the core share, multi-view "
                          "configs only; 0: off)")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
-                    help="PMC-derived HBM bytes per k_decode launch (from profiles/)")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r02_traffic_c2.json"),
+                    help="PMC-derived HBM bytes per step (committed profile of the same workload, "
+                         "scripts/traffic_from_pmc.py)")
     return ap.parse_args(argv)
 
 
@@ -161,12 +162,12 @@ def path_bytes(H, W, read_planes, n_points, maps):
     return read_planes * px + 3 * px + 15 * n_points + (9 * px if maps else 0)
 
 
-def decode_bytes(H, W, read_planes, maps):
+def decode_bytes(H, W, read_planes, maps, decide):
     """Algorithmic bytes of one k_decode pass over a view: the stack planes it
-    streams + the col/row int32 maps it writes (its 2-byte per-pixel records
-    for k_count / k_cloud are overhead, not counted; the mask map is written by
-    k_count)."""
-    return H * W * (read_planes + (8 if maps else 0))
+    streams + the col/row int32 maps it writes (+ the mask map on the decide
+    path, where k_decode applies the mask; else k_count writes it).  Its 2-byte
+    per-pixel records and point bits for k_cloud are overhead, not counted."""
+    return H * W * (read_planes + ((9 if decide else 8) if maps else 0))
 
 
 def cpu_baseline(stack_h, tex_h, calib, budget_s):
@@ -358,7 +359,8 @@ def main():
     # events' own cost amortised; the per-step events above include it).  Its
     # stack is larger than the 256 MB Infinity Cache, so the re-runs stream
     # from HBM like the steps (rocprofv3's per-dispatch average agrees)
-    _, n_groups, last_px = eng.last_launch_info()  # the launch group time_kernels re-runs
+    path_kind, n_groups, last_px = eng.last_launch_info()  # the launch group time_kernels re-runs
+    decide = path_kind == 1  # [k_stats] + k_decode (mask + point decision) + k_cloud
     v_last = last_px // (H * W)                 # views in the timed (last) group
     t_dec, t_cnt, t_cld = eng.time_kernels(max(a.steps, 10))
 
@@ -417,17 +419,23 @@ def main():
         rerun_ok = H * W * read_planes * v_last > 256 * 2 ** 20
         dec_avg_ms = t_dec if rerun_ok else decode_ms / max(nl, 1)
         v_roof = v_last if rerun_ok else V
-        ab = decode_bytes(H, W, read_planes, maps) * v_roof
+        ab = decode_bytes(H, W, read_planes, maps, decide) * v_roof
         achieved = ab / (dec_avg_ms * 1e-3) / 1e9
         path_b = path_bytes(H, W, read_planes, n_pts / V, maps) * V
-        traffic = None
+        path_gbps = path_b / (el / a.steps) / 1e9
+        # PMC bytes (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md)
+        # of the same command, from a committed profile -- not measured here
+        traffic = traffic_k = None
         if os.path.exists(a.traffic):
             try:
                 tj = json.load(open(a.traffic))
-                if tj.get("config") == a.config and tj.get("views") == V:
-                    traffic = tj.get("bytes_per_launch")
+                if tj.get("config") == a.config and tj.get("views") == V and tj.get("decide", False) == decide \
+                        and tj.get("xyz") == ("fast" if head_fast else "exact"):
+                    traffic = tj.get("bytes_per_step")
+                    traffic_k = tj.get("kernels", {}).get("k_decode")
             except (OSError, ValueError):
-                traffic = None
+                traffic = traffic_k = None
+        slots = ("k_decode", "k_stats", "k_cloud") if decide else ("k_decode", "k_count", "k_cloud")
         res = {
             "metric": "decoded+triangulated px/s",
             "value": value,
@@ -447,23 +455,38 @@ def main():
                                    + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
                        "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
                        "parallelism": f"views sharded over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_decode", "kernel_avg_ms": dec_avg_ms,
-                         "algorithmic_bytes_per_launch": ab,
-                         "bytes_note": f"{read_planes} stack planes read" + (" + col/row int32 maps written" if maps else "")
-                                       + f", per launch over {v_roof} view(s) (records are overhead); duration: "
-                                       + ("HIP events around back-to-back re-runs of the launch (sl_time_kernels)"
-                                          if rerun_ok else "HIP events around the kernel inside the steps")},
-            "path": {"algorithmic_bytes_per_step": path_b,
-                     "GBps": path_b / (el / a.steps) / 1e9,
-                     "kernel_avg_ms": {"k_decode": decode_ms / max(nl, 1), "k_count": count_ms / max(nl, 1),
-                                       "k_cloud": cloud_ms / max(nl, 1)},
+            "roofline": {"bound": "hbm", "scope": "whole path per step: every kernel of the step",
+                         "achieved": path_gbps, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": path_gbps / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": (f"PMC, {os.path.relpath(a.traffic, REPO)} (committed rocprofv3 "
+                                            "FETCH_SIZE x 2 + WRITE_SIZE of this command, per step)")
+                                           if traffic is not None else None,
+                         "algorithmic_bytes_per_step": path_b,
+                         "bytes_note": f"SURVEY.md 8(d): {read_planes} stack planes read + 3 B/px BGR texture + "
+                                       "15 B/point (f32 xyz + BGR)" + (" + 9 B/px col/row/mask maps" if maps else "")
+                                       + "; time: the step's wall time (barrier + synchronize on both sides)",
+                         "dominant_kernel": {
+                             "name": "k_decode", "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
+                             "avg_ms": dec_avg_ms, "algorithmic_bytes_per_launch": ab, "traffic": traffic_k,
+                             "bytes_note": f"{read_planes} stack planes read"
+                                           + ((" + col/row int32" + (" + mask" if decide else "") + " maps written")
+                                              if maps else "")
+                                           + f", per launch over {v_roof} view(s) (records, point bits are "
+                                             "overhead); duration: "
+                                           + ("HIP events around back-to-back re-runs of the launch "
+                                              "(sl_time_kernels)" if rerun_ok
+                                              else "HIP events around the kernel inside the steps")}},
+            "path": {"kind": "k_stats + k_decode (mask, point decision) + k_cloud" if decide
+                             else "k_decode + k_count + k_cloud",
+                     "launch_groups": n_groups,
+                     "kernel_avg_ms": {slots[0]: decode_ms / max(nl, 1), slots[1]: count_ms / max(nl, 1),
+                                       slots[2]: cloud_ms / max(nl, 1)},
                      "kernel_avg_ms_note": "HIP events around each kernel inside the steps (each event adds ~2-5 us)",
-                     "rerun_ms_last_group": {"k_decode": t_dec, "k_count": t_cnt, "k_cloud": t_cld,
+                     "rerun_ms_last_group": {slots[0]: t_dec, slots[1]: t_cnt, slots[2]: t_cld,
                                              "views": v_last,
-                                             "note": "back-to-back re-runs (sl_time_kernels); k_count / k_cloud "
-                                                     "inputs fit the 256 MB Infinity Cache, so theirs run warm"}},
+                                             "note": "back-to-back re-runs (sl_time_kernels); the inputs of the "
+                                                     "kernels after k_decode fit the 256 MB Infinity Cache, so "
+                                                     "theirs run warm"}},
             "cpu_baseline": cpu,
             "points_per_view": n_pts / V,
             "cloud_only_px_per_s": None if el_cloud is None else px_step * a.steps / el_cloud,

@@ -149,7 +149,10 @@ int sl_profile_enable(sl_ctx* ctx, int max_calls);
  * recorded calls since the last read, and their count; restarts recording. */
 int sl_profile_read(sl_ctx* ctx, double* decode_ms, double* count_ms, double* cloud_ms, int* calls);
 
-/* The last call's kernel path (0: k_decode + k_count + k_cloud), its number of
+/* The last call's kernel path -- 0: k_decode + k_count + k_cloud; 1: [k_stats]
+ * + k_decode + k_cloud, k_decode applying the mask and the point decision
+ * (frames with W % 16 == 0, W, H <= 4096 and Wp <= 2048; sl_profile_* and
+ * sl_time_kernels then report k_stats in the k_count slot) -- its number of
  * launch groups, and the pixels of its last launch group (what
  * sl_time_kernels re-runs).  Host only. */
 int sl_last_launch_info(sl_ctx* ctx, int* path, int64_t* launches, int64_t* last_launch_px);

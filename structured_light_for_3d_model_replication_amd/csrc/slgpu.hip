@@ -2369,7 +2369,7 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
 
 int sl_last_launch_info(sl_ctx* c, int* path, int64_t* launches, int64_t* last_launch_px) {
   if (!c) return SL_EINVAL;
-  if (path) *path = 0;
+  if (path) *path = c->last.decide ? 1 : 0;
   if (launches) *launches = c->last_launches;
   if (last_launch_px) *last_launch_px = c->last_launch_px;
   return SL_OK;
