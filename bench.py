@@ -247,6 +247,19 @@ def cpu_baselines(a, cfg, cfg_idx, gv, calib, rig):
            "sample": f"{n1} x {W}x{H} view(s), {st.shape[0]} planes, oracle/sl_oracle.py "
                      f"(NumPy restatement, bit-exact to reference fixtures), 1 process, {el1:.1f} s",
            **info}
+    # the oracle / reference speed ratio measured on one host with identical
+    # outputs (scripts/ref_vs_oracle_timing.py, build container): the
+    # reference's own code would run at about value / ratio here
+    ratio_f = os.path.join(REPO, "profiles", "r02_ref_vs_oracle_timing.json")
+    if os.path.exists(ratio_f):
+        try:
+            case = {1: "c1", 2: "c2", 3: "c3", 4: "c2", 5: "c2"}[cfg_idx]
+            r = next(x for x in json.load(open(ratio_f))["cases"] if x["case"].startswith(case))
+            out["reference_estimate"] = {"value": v1 / r["oracle_over_reference_speed"], "unit": "px/s",
+                                         "oracle_over_reference_speed": r["oracle_over_reference_speed"],
+                                         "source": f"profiles/r02_ref_vs_oracle_timing.json ({r['case']})"}
+        except (OSError, ValueError, KeyError, StopIteration):
+            pass
     procs = a.cpu_procs if a.cpu_procs else (info["core_share"] or min(os.cpu_count() or 1, 16))
     if a.cpu_procs != 0 and procs > 1 and (cfg["views"] > 1 or a.cpu_procs):
         vp, np_, elp = cpu_baseline_procs(st, tx, calib, procs, a.cpu_seconds)
