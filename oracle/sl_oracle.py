@@ -131,11 +131,32 @@ def pinhole_rays(valid_indices, h: int, w: int, cam_K):
     return rays
 
 
-def reconstruct_point_cloud(col_map, row_map, mask, texture, calib):
+def numerator_fixed(n, Oc):
+    """n.Oc for each column of n (3, M) in the order libslgpu.so fixes:
+    fma(n2, o2, fma(n0, o0, fl(n1 o1))) -- the order of the transposed
+    OpenBLAS dgemv np.dot runs for the reference's strided N.T
+    (sl_system.py:629-639) on the build host.  Exact rational arithmetic per
+    distinct plane, correctly rounded to f64 at each step."""
+    from fractions import Fraction as F
+    o = [float(v) for v in np.asarray(Oc, dtype=np.float64).reshape(3)]
+    cols = np.ascontiguousarray(n.T)
+    uniq, inv = np.unique(cols, axis=0, return_inverse=True)
+    vals = np.empty(len(uniq))
+    for i, (n0, n1, n2) in enumerate(uniq.tolist()):
+        p1 = float(F(n1) * F(o[1]))
+        f = float(F(n0) * F(o[0]) + F(p1))
+        vals[i] = float(F(n2) * F(o[2]) + F(f))
+    return vals[np.asarray(inv).reshape(-1)]
+
+
+def reconstruct_point_cloud(col_map, row_map, mask, texture, calib, oc_dot="blas"):
     """Ray/plane triangulation, sl_system.py:584-653.
 
     Returns (P float64 (N,3), C uint8 (N,3) BGR) in ascending pixel order.
-    ``row_map`` is accepted and unused, as in the reference.
+    ``row_map`` is accepted and unused, as in the reference.  ``oc_dot``:
+    "blas" computes n.Oc with np.dot as the reference does (:639) -- its
+    rounding follows the host's BLAS kernel, so it is host dependent when
+    Oc != 0; "fixed" uses the order of ``numerator_fixed``.
     """
     del row_map
     Nc = np.asarray(calib["Nc"])
@@ -156,7 +177,10 @@ def reconstruct_point_cloud(col_map, row_map, mask, texture, calib):
     n = pl[:, 0:3].T
     d = pl[:, 3]
     denom = np.sum(n * rays, axis=0)
-    numer = np.dot(n.T, Oc).flatten() + d
+    if oc_dot == "fixed":
+        numer = numerator_fixed(n, Oc) + d
+    else:
+        numer = np.dot(n.T, Oc).flatten() + d
     ok = np.abs(denom) > 1e-6
     t = -numer[ok] / denom[ok]
     P = Oc + rays[:, ok] * t
@@ -175,14 +199,14 @@ def apply_pose(points, pose):
 
 
 def decode_triangulate(images, texture, calib, n_cols=1920, n_rows=1080,
-                       mask_mode=MASK_ADAPTIVE, pose=None):
+                       mask_mode=MASK_ADAPTIVE, pose=None, oc_dot="blas"):
     """gray_decode + reconstruct_point_cloud in one call (generate_cloud body,
     sl_system.py:658-661).  ``texture`` is BGR (H,W,3); None -> file 0
     replicated (what cv2.imread colour returns for a single-channel file)."""
     col_map, row_map, mask = gray_decode_images(images, n_cols, n_rows, mask_mode)
     if texture is None:
         texture = np.repeat(np.asarray(images[0])[:, :, None], 3, axis=2)
-    P, C = reconstruct_point_cloud(col_map, row_map, mask, texture, calib)
+    P, C = reconstruct_point_cloud(col_map, row_map, mask, texture, calib, oc_dot)
     if pose is not None:
         P = apply_pose(P, pose)
     return col_map, row_map, mask, P, C

@@ -2066,18 +2066,19 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
     }
   }
   // per plane: (n0, n1, n2, n.Oc + d) -- numer of sl_system.py:639,
-  // np.dot(N.T, Oc).flatten() + d.  That np.dot is an OpenBLAS product whose
-  // bulk rows evaluate fma(n0, o0, n1 o1) + n2 o2 (measured in this image,
-  // DESIGN.md 5.1; its last M mod 8 rows take another kernel, so there the
-  // reference's own value depends on the pixel's rank and the CPU); then + d.
-  // With Oc = 0 (calibrate_final) every order gives d exactly.
+  // np.dot(N.T, Oc).flatten() + d.  N.T there is planes[:, 0:3] of the
+  // fancy-indexed (M, 4) C-ordered plane rows (:629-632), a strided
+  // row-major operand, so numpy hands OpenBLAS a transposed dgemv: one
+  // 3-term dot per row, evaluated fma(n2, o2, fma(n0, o0, n1 o1)) (measured
+  // in this image on every row); then + d.  With Oc = 0
+  // (calibrate_final) every order gives d exactly.
   std::vector<double> pl(4 * static_cast<size_t>(Wp));
   for (int i = 0; i < Wp; ++i) {
     const double* s = planes + 4 * static_cast<size_t>(i);
     pl[4 * i] = s[0];
     pl[4 * i + 1] = s[1];
     pl[4 * i + 2] = s[2];
-    pl[4 * i + 3] = (std::fma(s[0], Oc[0], s[1] * Oc[1]) + s[2] * Oc[2]) + s[3];
+    pl[4 * i + 3] = std::fma(s[2], Oc[2], std::fma(s[0], Oc[0], s[1] * Oc[1])) + s[3];
   }
   for (double* ptr : {c->d_planes, c->d_xn, c->d_yn, c->d_nc})
     if (ptr) HIP_TRY(c, hipFree(ptr));

@@ -125,11 +125,16 @@ def process_views(views, calib_data, *, n_cols=1920, n_rows=1080, device=None, w
 
 
 def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slots, keep, mask_mode="fixed",
-                      raise_errors=False):
+                      raise_errors=False, *, xyz_dtype=torch.float64, poses=None, device_sink=None, host=True):
     """Views grouped by (frame size, file count), each group through one
     ``pipeline.ViewPipeline``.  ``raise_errors``: a failing folder raises
     (SLSystem.generate_clouds) instead of being logged and skipped (the batch
-    GUI's loop)."""
+    GUI's loop).
+
+    Device-resident use (scan360): ``device_sink(folder, xyz, bgr)`` gets each
+    view's points as device tensors (valid during the call), ``poses``
+    ({folder: 4x4}) are applied inside k_cloud, and ``host=False`` keeps the
+    points in HBM (no D2H, no per-view PLY, nothing in the returned dict)."""
     files = {f: io.list_stack_files(f) for f in views}
     groups: dict = {}
     for f in views:
@@ -148,7 +153,7 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
         try:
             eng.set_calibration(calib_data, H, W)
             pipe = pipeline.ViewPipeline(eng, H=H, W=W, n_img=n_img, n_cols=n_cols, n_rows=n_rows,
-                                         mask_mode=mask_mode, xyz_dtype=torch.float64, slots=slots)
+                                         mask_mode=mask_mode, xyz_dtype=xyz_dtype, slots=slots)
         except (ValueError, IndexError) as e:
             for f in group:
                 error(f, e)
@@ -173,5 +178,12 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
                 log(f"Saved: {os.path.basename(f)}.ply ({len(xyz)} points)")
             out[f] = (xyz.copy(), bgr.copy()) if keep else ([], [])
 
-        pipe.run(len(group), fill, consume)
+        def on_device(i, xyz, bgr, group=group):
+            if group[i] not in failed:
+                device_sink(group[i], xyz, bgr)
+
+        gposes = None if poses is None else np.stack([np.asarray(poses[f], np.float64).reshape(4, 4)
+                                                      for f in group])
+        pipe.run(len(group), fill, consume if host else None,
+                 on_device=None if device_sink is None else on_device, poses=gposes)
     return {f: out[f] for f in views if f in out}

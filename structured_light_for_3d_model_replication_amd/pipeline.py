@@ -101,6 +101,14 @@ class ViewPipeline:
     they are, and must stay unchanged until ``consume`` has seen view i.
     ``consume(i, xyz, bgr)`` receives view i's points (numpy views of pinned
     memory, valid during the call) in view order, on the D2H thread.
+
+    Device-resident consumers: ``on_device(i, xyz, bgr)`` receives view i's
+    points as device tensors (slices of the slot's output, valid during the
+    call; the D2H stream is current, so copies the callback enqueues are
+    ordered before the slot is reused).  With ``consume=None`` the points never
+    leave HBM -- only the 16-byte view offsets come back, to size the slices.
+    ``poses`` (device or host [n_views, 4, 4] f64): view i is moved by
+    ``poses[i]`` inside k_cloud (the f64 pose epilogue of decode_triangulate).
     """
 
     def __init__(self, engine: core.Reconstructor, *, H: int, W: int, n_img: int, n_cols: int = 1920,
@@ -134,8 +142,15 @@ class ViewPipeline:
         self._esz = esz
         engine.reserve(1, px)
 
-    def run(self, n_views: int, fill, consume=None) -> PipelineStats:
+    def run(self, n_views: int, fill, consume=None, *, on_device=None, poses=None) -> PipelineStats:
         st = PipelineStats()
+        if poses is not None:
+            poses = torch.as_tensor(poses, dtype=torch.float64).reshape(-1, 4, 4)
+            if poses.shape[0] != n_views:
+                raise ValueError(f"{n_views} views but {poses.shape[0]} poses")
+            # uploaded once, before any compute-stream launch reads it
+            poses = poses.to(self.eng.device).contiguous()
+            torch.cuda.current_stream(self.eng.device).synchronize()
         free = queue.Queue()
         for k in range(self.slots):
             free.put(k)
@@ -158,12 +173,15 @@ class ViewPipeline:
                         self._hn[k].copy_(cl["view_offsets"], non_blocking=True)
                         self._d2h.synchronize()
                         n = int(self._hn[k][1] - self._hn[k][0])
-                        self._hx[k][:n].copy_(cl["xyz"][:n], non_blocking=True)
-                        self._hb[k][:n].copy_(cl["bgr"][:n], non_blocking=True)
+                        if on_device is not None:
+                            on_device(i, cl["xyz"][:n], cl["bgr"][:n])
+                        if consume is not None:
+                            self._hx[k][:n].copy_(cl["xyz"][:n], non_blocking=True)
+                            self._hb[k][:n].copy_(cl["bgr"][:n], non_blocking=True)
+                            st.d2h_bytes += n * (3 * self._esz + 3)
                         self._d2h.synchronize()
                     st.points += n
                     st.per_view_points.append(n)
-                    st.d2h_bytes += n * (3 * self._esz + 3)
                     if consume is not None:
                         t0 = time.perf_counter()
                         consume(i, self._hx[k][:n].numpy(), self._hb[k][:n].numpy())
@@ -204,7 +222,8 @@ class ViewPipeline:
                 self.eng.decode_triangulate(self._ds[k], self.n_cols, self.n_rows,
                                             texture=None if gray_tex else self._dt[k], mask_mode=self.mask_mode,
                                             maps=False, cloud=True, xyz_dtype=self.xyz_dtype,
-                                            fast_f32=self.fast_f32, stream=self._compute, out=self._out[k])
+                                            poses=None if poses is None else poses[i], fast_f32=self.fast_f32,
+                                            stream=self._compute, out=self._out[k])
                 done = torch.cuda.Event()
                 done.record(self._compute)
                 work.put((i, k, done))

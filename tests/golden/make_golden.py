@@ -119,9 +119,31 @@ def run_sl(ref, tmp, name, stack, cal, n_cols, n_rows, texture=None):
     return col, row, mask, tex, P, C
 
 
+def nonzero_oc_case(ref, tmp):
+    """Oc != 0 with a per-pixel Nc table: the numerator np.dot(N.T, Oc) + d
+    (sl_system.py:639) then depends on the BLAS's rounding order; the
+    calibration goes through savemat/loadmat so the arrays have the layout
+    the reference sees (loadmat's Fortran-ordered wPlaneCol)."""
+    rig, st, _ = render(48, 64, 1920, 1080, seed=23)
+    cal = synth.make_calibration(rig)
+    cal["Oc"] = np.array([[12.5], [-3.25], [40.0]])
+    mat = os.path.join(tmp, "calib_oc.mat")
+    scipy.io.savemat(mat, cal)
+    cal = {k: v for k, v in scipy.io.loadmat(mat).items() if not k.startswith("__")}
+    col, row, mask, tex, P, C = run_sl(ref, tmp, "oc", st, cal, 1920, 1080)
+    save_case("sl_nonzero_oc", {"mask_mode": "adaptive", "n_cols": 1920, "n_rows": 1080, "func": "sl"},
+              stack=st, texture=tex, col_map=col, row_map=row, mask=mask, P=P, C=C, **calib_arrays(cal))
+
+
 def main():
     ref = load_reference()
     tmp = tempfile.mkdtemp(prefix="golden_")
+    if "--only-nonzero-oc" in sys.argv:  # add the one case without rewriting the others
+        try:
+            nonzero_oc_case(ref, tmp)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     for f in glob.glob(os.path.join(HERE, "*.npz")) + glob.glob(os.path.join(HERE, "*.ply")):
         os.remove(f)
     try:
@@ -279,6 +301,7 @@ def main():
                 errs[tag] = type(e).__name__
         save_case("errors", {"errors": errs, "n_cols": 16, "n_rows": 8}, stack=st)
         print("errors:", errs)
+        nonzero_oc_case(ref, tmp)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

@@ -87,8 +87,12 @@ def test_scan_distributed_gloo_world2(tmp_path, V):
 
 @pytest.mark.gpu
 def test_scan_distributed_gpu_world1(tmp_path):
-    """The real per-rank path (streamed GPU pipeline, device pose transform,
-    RCCL process group of one, merge post-processing) vs the oracle."""
+    """The real per-rank path (streamed GPU pipeline, pose applied on the
+    device, RCCL process group of one, merge post-processing) vs the oracle:
+    the default float32 gather is the correctly rounded float32 of the
+    oracle's f64 point, the f64 gather is bit-identical to it, and the
+    device-resident mode (no per-view PLY, pose inside k_cloud, no host copy)
+    gives the same bits as the PLY-writing mode."""
     from structured_light_for_3d_model_replication_amd import merge, ply, scan360
     V = 4
     parent = str(tmp_path / "scan")
@@ -97,24 +101,71 @@ def test_scan_distributed_gpu_world1(tmp_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    quiet = dict(n_cols=RIG["Wp"], n_rows=RIG["Hp"], log=lambda *a: None)
     try:
-        out = str(tmp_path / "merged.ply")
-        P, C, counts = scan360.scan_distributed(parent, calib, poses=poses, n_cols=RIG["Wp"], n_rows=RIG["Hp"],
-                                                log=lambda *a: None)
         views = sorted(os.path.join(parent, f"view_{v:02d}") for v in range(V))
         ref = _oracle_views(views, calib, poses)
-        np.testing.assert_array_equal(P.cpu().numpy(), np.concatenate([p.numpy() for p, _ in ref]))
-        np.testing.assert_array_equal(C.cpu().numpy(), np.concatenate([c.numpy() for _, c in ref]))
+        P_ref = np.concatenate([p.numpy() for p, _ in ref])
+        C_ref = np.concatenate([c.numpy() for _, c in ref])
+
+        P, C, counts = scan360.scan_distributed(parent, calib, poses=poses, **quiet)
+        assert P.dtype == torch.float32
+        np.testing.assert_array_equal(P.cpu().numpy(), P_ref.astype(np.float32))
+        np.testing.assert_array_equal(C.cpu().numpy(), C_ref)
         assert counts == [len(P)]
-        for f in views:
-            assert os.path.exists(os.path.join(f, os.path.basename(f) + ".ply"))
-        Pm, Cm, _ = scan360.scan_distributed(parent, calib, poses=poses, n_cols=RIG["Wp"], n_rows=RIG["Hp"],
-                                             voxel_size=5.0, merge_output=out, write_views=False,
-                                             log=lambda *a: None)
+        for f in views:  # camera-frame per-view files, as the reference writes them
+            Pv, _ = ply.read_ply(os.path.join(f, os.path.basename(f) + ".ply"))
+            assert len(Pv) == len(ref[views.index(f)][0])
+
+        P64, C64, _ = scan360.scan_distributed(parent, calib, poses=poses, xyz_dtype=torch.float64,
+                                               write_views=False, **quiet)
+        assert P64.dtype == torch.float64
+        np.testing.assert_array_equal(P64.cpu().numpy(), P_ref)
+        np.testing.assert_array_equal(C64.cpu().numpy(), C_ref)
+
+        Pd, Cd, _ = scan360.scan_distributed(parent, calib, poses=poses, write_views=False, native_gather=True,
+                                             **quiet)
+        np.testing.assert_array_equal(Pd.cpu().numpy(), P.cpu().numpy())
+        np.testing.assert_array_equal(Cd.cpu().numpy(), C_ref)
+
+        out = str(tmp_path / "merged.ply")
+        Pm, Cm, _ = scan360.scan_distributed(parent, calib, poses=poses, voxel_size=5.0, merge_output=out,
+                                             write_views=False, **quiet)
         Pe, Ce = merge.postprocess(P, C, 5.0)
         np.testing.assert_array_equal(Pm.cpu().numpy(), Pe.cpu().numpy())
+        np.testing.assert_array_equal(Cm.cpu().numpy(), Ce.cpu().numpy())
         Pr, Cr = ply.read_ply(out)  # binary PLY: float32 xyz
         np.testing.assert_array_equal(np.asarray(Pr, np.float32), Pm.cpu().numpy().astype(np.float32))
         np.testing.assert_array_equal(np.asarray(Cr), Cm.cpu().numpy())
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_pipeline_device_sink_keeps_points_in_hbm(tmp_path):
+    """ViewPipeline(on_device=..., consume=None): no point is copied to the
+    host (d2h_bytes == 0) and the device clouds equal the host-consumed ones;
+    poses given to run() equal the oracle's posed points."""
+    from structured_light_for_3d_model_replication_amd import core, io, pipeline
+    V = 3
+    parent = str(tmp_path / "scan")
+    calib = _write_scan(parent, V)
+    views = sorted(os.path.join(parent, f"view_{v:02d}") for v in range(V))
+    poses = np.stack([synth.turntable_pose(30.0 * v) for v in range(V)])
+    eng = core.engine("cuda:0")
+    eng.set_calibration(calib, RIG["H"], RIG["W"])
+    files = [io.list_stack_files(f) for f in views]
+    pipe = pipeline.ViewPipeline(eng, H=RIG["H"], W=RIG["W"], n_img=len(files[0]), n_cols=RIG["Wp"],
+                                 n_rows=RIG["Hp"], mask_mode="fixed", xyz_dtype=torch.float64)
+    got = {}
+
+    def fill(i, stack, tex):
+        return io.fill_stack(files[i], stack.numpy(), tex.numpy())
+
+    st = pipe.run(V, fill, None, on_device=lambda i, x, b: got.__setitem__(i, (x.clone(), b.clone())),
+                  poses=poses)
+    assert st.d2h_bytes == 0 and st.views == V
+    ref = _oracle_views(views, calib, list(poses))
+    for i in range(V):
+        np.testing.assert_array_equal(got[i][0].cpu().numpy(), ref[i][0].numpy())
+        np.testing.assert_array_equal(got[i][1].cpu().numpy(), ref[i][1].numpy())
