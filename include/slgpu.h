@@ -180,8 +180,9 @@ int sl_write_ply(const char* path, const void* xyz, int xyz_dtype, const uint8_t
 
 /* Binary little-endian PLY with the same header properties (float x y z,
  * uchar red green blue; colour swapped from BGR): 15-byte records, xyz rounded
- * to float32 when xyz_dtype is SL_XYZ_F64.  What Open3D's write_point_cloud
- * produces by default, for the merge stage (processing.py:116-182). */
+ * to float32 when xyz_dtype is SL_XYZ_F64.  A compact binary form of the
+ * reference's ASCII file (the merged cloud's Open3D-layout file, double xyz
+ * and normals, is ply.save_ply_open3d). */
 int sl_write_ply_binary(const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n,
                         int threads);
 
@@ -214,6 +215,16 @@ int sl_select_by_index(sl_ctx* ctx, const double* xyz, const uint8_t* bgr, const
 /* In place p' = M p for a row-major 4x4 pose (device), rows in the order
  * ((m0 x + m1 y) + m2 z) + m3 -- PointCloud::Transform.  Asynchronous. */
 int sl_transform_points(sl_ctx* ctx, double* xyz, int64_t n, const double* pose, void* stream);
+
+/* PointCloud::EstimateNormals(KDTreeSearchParamHybrid(radius, max_nn)) on a
+ * cloud without normals (processing.py:178: radius = 2 voxel, max_nn = 30):
+ * per point, the neighbours with ((dx^2 + dy^2) + dz^2) < radius^2 (itself
+ * included) in ascending (distance, index), the first max_nn; covariance from
+ * their cumulants (identity below 3 neighbours); normal = Open3D's
+ * FastEigen3x3 eigenvector of the smallest eigenvalue, (0, 0, 1) when zero ->
+ * normals [n][3] f64 (device).  max_nn <= 32.  Blocking on `stream`. */
+int sl_estimate_normals(sl_ctx* ctx, const double* xyz, int64_t n, double radius, int max_nn, double* normals,
+                        void* stream);
 
 /* Release the scratch buffers the merge entry points keep pooled for `device`
  * (kept otherwise for the process's lifetime, at most 16 GiB per device);

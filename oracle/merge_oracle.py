@@ -107,3 +107,285 @@ def remove_statistical_outlier(points, nb_neighbors, std_ratio):
     """-> (indices kept, per-point mean kNN distance)."""
     avg = knn_mean_distances(points, nb_neighbors)
     return statistical_outlier_indices(avg, std_ratio), avg
+
+
+# --------------------------------------------------------------------------
+# PointCloud::EstimateNormals(KDTreeSearchParamHybrid(radius, max_nn)), the
+# call server/processing.py:178 makes on the merged cloud (radius = 2 voxel,
+# max_nn = 30), restated from Open3D's published source
+# (geometry/EstimateNormals.cpp, utility/Eigen.cpp ComputeCovariance,
+# KDTreeFlann::SearchHybrid):
+#
+# - neighbours: every point with ((dx*dx + dy*dy) + dz*dz) < radius^2 (the
+#   point itself included), ascending distance, the first max_nn (ties by
+#   ascending index here; nanoflann's std::sort leaves them unordered);
+# - fewer than 3 neighbours -> covariance = identity, else the cumulants
+#   (sum x, y, z, xx, xy, xz, yy, yz, zz in neighbour order) / count and
+#   covariance = E[ab] - E[a] E[b];
+# - normal = FastEigen3x3(covariance) (Geometric Tools' robust symmetric 3x3
+#   eigen solver: eigenvector of the smallest eigenvalue); zero -> (0, 0, 1).
+#
+# FastEigen3x3 calls std::acos / std::cos.  Their last-ulp behaviour is the
+# C library's, so the GPU path and this restatement both use the fdlibm
+# algorithms below (only +, -, *, /, sqrt and bit masking: bit-identical on
+# any IEEE machine); they differ from glibc's by at most an ulp or so.  Parity
+# with Open3D stays unpinned (no Open3D in this image).
+# --------------------------------------------------------------------------
+import math  # noqa: E402
+import struct  # noqa: E402
+
+_PIO2_HI = 1.57079632679489655800e+00
+_PIO2_LO = 6.12323399573676603587e-17
+_PI = 3.14159265358979311600e+00
+_PS = (1.66666666666666657415e-01, -3.25565818622400915405e-01, 2.01212532134862925881e-01,
+       -4.00555345006794114027e-02, 7.91534994289814532176e-04, 3.47933107596021167570e-05)
+_QS = (-2.40339491173441421878e+00, 2.02094576023350569471e+00, -6.88283971605453293030e-01,
+       7.70381505559019352791e-02)
+_C = (4.16666666666666019037e-02, -1.38888888888741095749e-03, 2.48015872894767294178e-05,
+      -2.75573143513906633035e-07, 2.08757232129817482790e-09, -1.13596475577881948265e-11)
+_S = (-1.66666666666666324348e-01, 8.33333333332248946124e-03, -1.98412698298579493134e-04,
+      2.75573137070700676789e-06, -2.50507602534068634195e-08, 1.58969099521155010221e-10)
+_INVPIO2 = 6.36619772367581382433e-01
+_PIO2_1 = 1.57079632673412561417e+00
+_PIO2_1T = 6.07710050650619224932e-11
+
+
+def _low_word_zero(x):
+    (u,) = struct.unpack("<Q", struct.pack("<d", x))
+    return struct.unpack("<d", struct.pack("<Q", u & 0xFFFFFFFF00000000))[0]
+
+
+def _acos_rational(z):
+    p = z * (_PS[0] + z * (_PS[1] + z * (_PS[2] + z * (_PS[3] + z * (_PS[4] + z * _PS[5])))))
+    q = 1.0 + z * (_QS[0] + z * (_QS[1] + z * (_QS[2] + z * _QS[3])))
+    return p / q
+
+
+def acos_det(x):
+    """fdlibm e_acos.c for x in [-1, 1]."""
+    ax = abs(x)
+    if ax >= 1.0:
+        return 0.0 if x == 1.0 else (_PI if x == -1.0 else float("nan"))
+    if ax < 0.5:
+        if ax <= 2.0 ** -57:
+            return _PIO2_HI + _PIO2_LO
+        r = _acos_rational(x * x)
+        return _PIO2_HI - (x - (_PIO2_LO - x * r))
+    if x < 0.0:
+        z = (1.0 + x) * 0.5
+        s = math.sqrt(z)
+        r = _acos_rational(z)
+        w = r * s - _PIO2_LO
+        return _PI - 2.0 * (s + w)
+    z = (1.0 - x) * 0.5
+    s = math.sqrt(z)
+    df = _low_word_zero(s)
+    c = (z - df * df) / (s + df)
+    r = _acos_rational(z)
+    w = r * s + c
+    return 2.0 * (df + w)
+
+
+def _kcos(x, y):
+    z = x * x
+    w = z * z
+    r = z * (_C[0] + z * (_C[1] + z * _C[2])) + w * w * (_C[3] + z * (_C[4] + z * _C[5]))
+    hz = 0.5 * z
+    w = 1.0 - hz
+    return w + (((1.0 - w) - hz) + (z * r - x * y))
+
+
+def _ksin(x, y):
+    z = x * x
+    w = z * z
+    r = _S[1] + z * (_S[2] + z * _S[3]) + z * w * (_S[4] + z * _S[5])
+    v = z * x
+    return x - ((z * (0.5 * y - v * r) - y) - v * _S[0])
+
+
+def cos_det(x):
+    """fdlibm s_cos.c for x in [0, 4]: one-constant Cody-Waite reduction by
+    pi/2 (n * _PIO2_1 is exact for n < 2^20), then the kernels."""
+    if x <= 0.7853981633974483:
+        return _kcos(x, 0.0)
+    n = math.floor(x * _INVPIO2 + 0.5)
+    fn = float(n)
+    r = x - fn * _PIO2_1
+    w = fn * _PIO2_1T
+    y0 = r - w
+    y1 = (r - y0) - w
+    q = n & 3
+    if q == 0:
+        return _kcos(y0, y1)
+    if q == 1:
+        return -_ksin(y0, y1)
+    if q == 2:
+        return -_kcos(y0, y1)
+    return _ksin(y0, y1)
+
+
+def _cross(a, b):
+    return (a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0])
+
+
+def _dot(a, b):
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]
+
+
+def _evec0(A, e):
+    r0 = (A[0][0] - e, A[0][1], A[0][2])
+    r1 = (A[0][1], A[1][1] - e, A[1][2])
+    r2 = (A[0][2], A[1][2], A[2][2] - e)
+    c01, c02, c12 = _cross(r0, r1), _cross(r0, r2), _cross(r1, r2)
+    d0, d1, d2 = _dot(c01, c01), _dot(c02, c02), _dot(c12, c12)
+    dmax, imax = d0, 0
+    if d1 > dmax:
+        dmax, imax = d1, 1
+    if d2 > dmax:
+        imax = 2
+    v, d = ((c01, d0), (c02, d1), (c12, d2))[imax]
+    s = math.sqrt(d)
+    return (v[0] / s, v[1] / s, v[2] / s)
+
+
+def _evec1(A, ev0, e1):
+    if abs(ev0[0]) > abs(ev0[1]):
+        inv = 1.0 / math.sqrt(ev0[0] * ev0[0] + ev0[2] * ev0[2])
+        U = (-ev0[2] * inv, 0.0, ev0[0] * inv)
+    else:
+        inv = 1.0 / math.sqrt(ev0[1] * ev0[1] + ev0[2] * ev0[2])
+        U = (0.0, ev0[2] * inv, -ev0[1] * inv)
+    V = _cross(ev0, U)
+    AU = (A[0][0] * U[0] + A[0][1] * U[1] + A[0][2] * U[2],
+          A[0][1] * U[0] + A[1][1] * U[1] + A[1][2] * U[2],
+          A[0][2] * U[0] + A[1][2] * U[1] + A[2][2] * U[2])
+    AV = (A[0][0] * V[0] + A[0][1] * V[1] + A[0][2] * V[2],
+          A[0][1] * V[0] + A[1][1] * V[1] + A[1][2] * V[2],
+          A[0][2] * V[0] + A[1][2] * V[1] + A[2][2] * V[2])
+    m00 = U[0] * AU[0] + U[1] * AU[1] + U[2] * AU[2] - e1
+    m01 = U[0] * AV[0] + U[1] * AV[1] + U[2] * AV[2]
+    m11 = V[0] * AV[0] + V[1] * AV[1] + V[2] * AV[2] - e1
+    a00, a01, a11 = abs(m00), abs(m01), abs(m11)
+    if a00 >= a11:
+        if max(a00, a01) > 0.0:
+            if a00 >= a01:
+                m01 /= m00
+                m00 = 1.0 / math.sqrt(1.0 + m01 * m01)
+                m01 *= m00
+            else:
+                m00 /= m01
+                m01 = 1.0 / math.sqrt(1.0 + m00 * m00)
+                m00 *= m01
+            return (m01 * U[0] - m00 * V[0], m01 * U[1] - m00 * V[1], m01 * U[2] - m00 * V[2])
+        return U
+    if max(a11, a01) > 0.0:
+        if a11 >= a01:
+            m01 /= m11
+            m11 = 1.0 / math.sqrt(1.0 + m01 * m01)
+            m01 *= m11
+        else:
+            m11 /= m01
+            m01 = 1.0 / math.sqrt(1.0 + m11 * m11)
+            m11 *= m01
+        return (m11 * U[0] - m01 * V[0], m11 * U[1] - m01 * V[1], m11 * U[2] - m01 * V[2])
+    return U
+
+
+def fast_eigen3x3(C):
+    """Open3D's FastEigen3x3: unit eigenvector of the smallest eigenvalue of
+    the symmetric 3x3 C (tuple of rows); (0, 0, 0) for C == 0."""
+    mx = max(C[0][0], C[0][1], C[0][2], C[1][0], C[1][1], C[1][2], C[2][0], C[2][1], C[2][2])
+    if mx == 0.0:
+        return (0.0, 0.0, 0.0)
+    A = [[C[r][k] / mx for k in range(3)] for r in range(3)]
+    norm = A[0][1] * A[0][1] + A[0][2] * A[0][2] + A[1][2] * A[1][2]
+    if norm > 0.0:
+        q = (A[0][0] + A[1][1] + A[2][2]) / 3.0
+        b00, b11, b22 = A[0][0] - q, A[1][1] - q, A[2][2] - q
+        p = math.sqrt((b00 * b00 + b11 * b11 + b22 * b22 + norm * 2.0) / 6.0)
+        c00 = b11 * b22 - A[1][2] * A[1][2]
+        c01 = A[0][1] * b22 - A[1][2] * A[0][2]
+        c02 = A[0][1] * A[1][2] - b11 * A[0][2]
+        det = (b00 * c00 - A[0][1] * c01 + A[0][2] * c02) / (p * p * p)
+        half_det = min(max(det * 0.5, -1.0), 1.0)
+        angle = acos_det(half_det) / 3.0
+        two_thirds_pi = 2.09439510239319549
+        beta2 = cos_det(angle) * 2.0
+        beta0 = cos_det(angle + two_thirds_pi) * 2.0
+        beta1 = -(beta0 + beta2)
+        ev = (q + p * beta0, q + p * beta1, q + p * beta2)
+        if half_det >= 0.0:
+            e2 = _evec0(A, ev[2])
+            if ev[2] < ev[0] and ev[2] < ev[1]:
+                return e2
+            e1 = _evec1(A, e2, ev[1])
+            if ev[1] < ev[0] and ev[1] < ev[2]:
+                return e1
+            return _cross(e1, e2)
+        e0 = _evec0(A, ev[0])
+        if ev[0] < ev[1] and ev[0] < ev[2]:
+            return e0
+        e1 = _evec1(A, e0, ev[1])
+        if ev[1] < ev[0] and ev[1] < ev[2]:
+            return e1
+        return _cross(e0, e1)
+    if C[0][0] < C[1][1] and C[0][0] < C[2][2]:
+        return (1.0, 0.0, 0.0)
+    if C[1][1] < C[0][0] and C[1][1] < C[2][2]:
+        return (0.0, 1.0, 0.0)
+    return (0.0, 0.0, 1.0)
+
+
+def hybrid_neighbours(points, radius, max_nn):
+    """KDTreeFlann::SearchHybrid for every point -> list of index arrays
+    (ascending (distance, index)), exact distances in nanoflann's order
+    (which compares against radius * radius: a negative radius acts as its
+    absolute value)."""
+    from scipy.spatial import cKDTree
+    P = np.asarray(points, dtype=np.float64)
+    r2 = radius * radius
+    cand = cKDTree(P).query_ball_point(P, abs(radius) * (1.0 + 1e-9) + 1e-300)
+    out = []
+    for i, c in enumerate(cand):
+        c = np.asarray(sorted(c), dtype=np.int64)
+        d = P[i] - P[c]
+        d2 = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+        keep = d2 < r2
+        c, d2 = c[keep], d2[keep]
+        o = np.lexsort((c, d2))
+        out.append(c[o][:max_nn])
+    return out
+
+
+def estimate_normals(points, radius, max_nn=30):
+    """PointCloud::EstimateNormals(KDTreeSearchParamHybrid(radius, max_nn))
+    on a cloud without normals -> (N, 3) float64."""
+    P = np.asarray(points, dtype=np.float64)
+    out = np.empty_like(P)
+    for i, nb in enumerate(hybrid_neighbours(P, radius, max_nn)):
+        if len(nb) >= 3:
+            s = [0.0] * 9
+            for j in nb.tolist():
+                x, y, z = P[j].tolist()
+                s[0] += x
+                s[1] += y
+                s[2] += z
+                s[3] += x * x
+                s[4] += x * y
+                s[5] += x * z
+                s[6] += y * y
+                s[7] += y * z
+                s[8] += z * z
+            k = float(len(nb))
+            s = [v / k for v in s]
+            c01 = s[4] - s[0] * s[1]
+            c02 = s[5] - s[0] * s[2]
+            c12 = s[7] - s[1] * s[2]
+            C = ((s[3] - s[0] * s[0], c01, c02), (c01, s[6] - s[1] * s[1], c12), (c02, c12, s[8] - s[2] * s[2]))
+        else:
+            C = ((1.0, 0.0, 0.0), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
+        n = fast_eigen3x3(C)
+        if math.sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]) == 0.0:
+            n = (0.0, 0.0, 1.0)
+        out[i] = n
+    return out

@@ -4,7 +4,9 @@ The workload is V posed 4K views triangulated in one launch (f64 xyz, turntable
 poses), merged in view order.  On it, one JSON line reports:
 
 - ``voxel_down_sample(voxel)``;
-- ``remove_statistical_outlier(20, 2.0)`` on the downsampled cloud.
+- ``remove_statistical_outlier(20, 2.0)`` on the downsampled cloud;
+- ``estimate_normals(KDTreeSearchParamHybrid(2 voxel, 30))`` on the kept cloud
+  (processing.py:178).
 
 Both are device time around the blocking calls.  A CPU reference runs beside
 them on a bounded sample, 1 thread: the NumPy voxel oracle, and scipy's
@@ -32,6 +34,7 @@ def main():
     ap.add_argument("--voxel", type=float, default=1.0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-sample", type=int, default=400_000)
+    ap.add_argument("--cpu-normals-sample", type=int, default=20_000)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rig = synth.Rig(H=2160, W=3840, Wp=1920, Hp=1080)
@@ -68,6 +71,9 @@ def main():
     t_vox, (Q, Cq) = timed(lambda: merge.voxel_down_sample(P, C, a.voxel))
     m = Q.shape[0]
     t_sor, (ind, _) = timed(lambda: merge.remove_statistical_outlier(Q, 20, 2.0))
+    K, _ = merge.select_by_index(Q, None, ind)
+    k = K.shape[0]
+    t_nrm, _ = timed(lambda: merge.estimate_normals(K, 2 * a.voxel, 30))
 
     # CPU reference on a bounded sample, 1 thread
     from scipy.spatial import cKDTree
@@ -82,13 +88,20 @@ def main():
     t0 = time.perf_counter()
     cKDTree(sq).query(sq, k=20, workers=1)
     cpu_knn = len(sq) / (time.perf_counter() - t0)
+    sn = K[: min(k, a.cpu_normals_sample)].cpu().numpy()
+    t0 = time.perf_counter()
+    mo.estimate_normals(sn, 2 * a.voxel, 30)
+    cpu_nrm = len(sn) / (time.perf_counter() - t0)
     print(json.dumps({
         "workload": f"{a.views} posed 3840x2160 views merged: {n} points (f64), voxel {a.voxel}",
         "points_in": n, "points_voxel": m, "points_kept": int(ind.shape[0]),
         "voxel_down_sample_ms": 1e3 * t_vox, "voxel_Mpts_per_s": n / t_vox / 1e6,
         "statistical_outliers_ms": 1e3 * t_sor, "sor_Mpts_per_s": m / t_sor / 1e6,
+        "normals_ms": 1e3 * t_nrm, "normals_Mpts_per_s": k / t_nrm / 1e6,
         "cpu_baseline": {"voxel_oracle_Mpts_per_s": cpu_vox / 1e6, "ckdtree_knn20_Mpts_per_s": cpu_knn / 1e6,
-                         "cores": 1, "sample": f"{len(sp)} / {len(sq)} points"},
+                         "normals_oracle_Mpts_per_s": cpu_nrm / 1e6,
+                         "cores": 1, "sample": f"{len(sp)} / {len(sq)} / {len(sn)} points (normals: the "
+                                               "pure-Python oracle, a restatement, not Open3D's C++)"},
     }))
 
 

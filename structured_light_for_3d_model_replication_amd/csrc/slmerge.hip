@@ -874,6 +874,331 @@ __global__ __launch_bounds__(kT) void k_transform(double* xyz, int64_t n, const 
   for (int r = 0; r < 3; ++r) xyz[3 * i + r] = ((m[4 * r] * x + m[4 * r + 1] * y) + m[4 * r + 2] * z) + m[4 * r + 3];
 }
 
+// -------------------------------------------------------------- normals ----
+// PointCloud::EstimateNormals(KDTreeSearchParamHybrid(radius, max_nn)) --
+// processing.py:178 on the merged cloud (radius 2 voxel, max_nn 30):
+// neighbours = the points with ((dx^2 + dy^2) + dz^2) < radius^2 (itself
+// included), ascending (distance, index), the first max_nn; fewer than 3 ->
+// identity covariance, else cumulants in neighbour order / count ->
+// E[ab] - E[a]E[b]; normal = FastEigen3x3 (Geometric Tools' robust symmetric
+// 3x3 solver, Open3D utility/Eigen.cpp); a zero result -> (0, 0, 1).
+// FastEigen3x3's acos / cos are the fdlibm algorithms (only IEEE basic ops,
+// so the same bits as oracle/merge_oracle.py on any host; <= 1 ulp from the
+// exact value on the ranges used).
+namespace nrm {
+
+constexpr double kPio2Hi = 1.57079632679489655800e+00, kPio2Lo = 6.12323399573676603587e-17;
+constexpr double kPi = 3.14159265358979311600e+00;
+constexpr double kInvPio2 = 6.36619772367581382433e-01, kPio2_1 = 1.57079632673412561417e+00,
+                 kPio2_1t = 6.07710050650619224932e-11;
+
+__device__ __forceinline__ double acos_rational(double z) {
+  const double p = z * (1.66666666666666657415e-01 +
+                        z * (-3.25565818622400915405e-01 +
+                             z * (2.01212532134862925881e-01 +
+                                  z * (-4.00555345006794114027e-02 +
+                                       z * (7.91534994289814532176e-04 + z * 3.47933107596021167570e-05)))));
+  const double q = 1.0 + z * (-2.40339491173441421878e+00 +
+                              z * (2.02094576023350569471e+00 +
+                                   z * (-6.88283971605453293030e-01 + z * 7.70381505559019352791e-02)));
+  return p / q;
+}
+
+__device__ double acos_det(double x) {
+  const double ax = fabs(x);
+  if (ax >= 1.0) return x == 1.0 ? 0.0 : (x == -1.0 ? kPi : __builtin_nan(""));
+  if (ax < 0.5) {
+    if (ax <= 6.938893903907228e-18) return kPio2Hi + kPio2Lo;  // 2^-57
+    const double r = acos_rational(x * x);
+    return kPio2Hi - (x - (kPio2Lo - x * r));
+  }
+  if (x < 0.0) {
+    const double z = (1.0 + x) * 0.5;
+    const double s = sqrt(z);
+    const double r = acos_rational(z);
+    const double w = r * s - kPio2Lo;
+    return kPi - 2.0 * (s + w);
+  }
+  const double z = (1.0 - x) * 0.5;
+  const double s = sqrt(z);
+  const double df = __longlong_as_double(__double_as_longlong(s) & static_cast<long long>(0xFFFFFFFF00000000ull));
+  const double c = (z - df * df) / (s + df);
+  const double r = acos_rational(z);
+  const double w = r * s + c;
+  return 2.0 * (df + w);
+}
+
+__device__ __forceinline__ double kcos(double x, double y) {
+  const double z = x * x;
+  double w = z * z;
+  const double r = z * (4.16666666666666019037e-02 + z * (-1.38888888888741095749e-03 + z * 2.48015872894767294178e-05)) +
+                   w * w * (-2.75573143513906633035e-07 + z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11));
+  const double hz = 0.5 * z;
+  w = 1.0 - hz;
+  return w + (((1.0 - w) - hz) + (z * r - x * y));
+}
+
+__device__ __forceinline__ double ksin(double x, double y) {
+  const double z = x * x;
+  const double w = z * z;
+  const double r = 8.33333333332248946124e-03 + z * (-1.98412698298579493134e-04 + z * 2.75573137070700676789e-06) +
+                   z * w * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10);
+  const double v = z * x;
+  return x - ((z * (0.5 * y - v * r) - y) - v * -1.66666666666666324348e-01);
+}
+
+// x in [0, 4]
+__device__ double cos_det(double x) {
+  if (x <= 0.7853981633974483) return kcos(x, 0.0);
+  const double fn = floor(x * kInvPio2 + 0.5);
+  const int n = static_cast<int>(fn);
+  const double r = x - fn * kPio2_1;
+  const double w = fn * kPio2_1t;
+  const double y0 = r - w;
+  const double y1 = (r - y0) - w;
+  switch (n & 3) {
+    case 0: return kcos(y0, y1);
+    case 1: return -ksin(y0, y1);
+    case 2: return -kcos(y0, y1);
+    default: return ksin(y0, y1);
+  }
+}
+
+struct V3 {
+  double x, y, z;
+};
+
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+// A: symmetric, entries a00 a01 a02 a11 a12 a22
+struct S3 {
+  double a00, a01, a02, a11, a12, a22;
+};
+
+__device__ V3 evec0(const S3& A, double e) {
+  const V3 r0{A.a00 - e, A.a01, A.a02}, r1{A.a01, A.a11 - e, A.a12}, r2{A.a02, A.a12, A.a22 - e};
+  const V3 c01 = cross(r0, r1), c02 = cross(r0, r2), c12 = cross(r1, r2);
+  const double d0 = dot(c01, c01), d1 = dot(c02, c02), d2 = dot(c12, c12);
+  double dmax = d0;
+  int imax = 0;
+  if (d1 > dmax) {
+    dmax = d1;
+    imax = 1;
+  }
+  if (d2 > dmax) imax = 2;
+  const V3 v = imax == 0 ? c01 : (imax == 1 ? c02 : c12);
+  const double sq = sqrt(imax == 0 ? d0 : (imax == 1 ? d1 : d2));
+  return {v.x / sq, v.y / sq, v.z / sq};
+}
+
+__device__ V3 evec1(const S3& A, V3 e0, double e1) {
+  V3 U;
+  if (fabs(e0.x) > fabs(e0.y)) {
+    const double inv = 1.0 / sqrt(e0.x * e0.x + e0.z * e0.z);
+    U = {-e0.z * inv, 0.0, e0.x * inv};
+  } else {
+    const double inv = 1.0 / sqrt(e0.y * e0.y + e0.z * e0.z);
+    U = {0.0, e0.z * inv, -e0.y * inv};
+  }
+  const V3 V = cross(e0, U);
+  const V3 AU{A.a00 * U.x + A.a01 * U.y + A.a02 * U.z, A.a01 * U.x + A.a11 * U.y + A.a12 * U.z,
+              A.a02 * U.x + A.a12 * U.y + A.a22 * U.z};
+  const V3 AV{A.a00 * V.x + A.a01 * V.y + A.a02 * V.z, A.a01 * V.x + A.a11 * V.y + A.a12 * V.z,
+              A.a02 * V.x + A.a12 * V.y + A.a22 * V.z};
+  double m00 = U.x * AU.x + U.y * AU.y + U.z * AU.z - e1;
+  double m01 = U.x * AV.x + U.y * AV.y + U.z * AV.z;
+  double m11 = V.x * AV.x + V.y * AV.y + V.z * AV.z - e1;
+  const double a00 = fabs(m00), a01 = fabs(m01), a11 = fabs(m11);
+  if (a00 >= a11) {
+    if (fmax(a00, a01) > 0.0) {
+      if (a00 >= a01) {
+        m01 /= m00;
+        m00 = 1.0 / sqrt(1.0 + m01 * m01);
+        m01 *= m00;
+      } else {
+        m00 /= m01;
+        m01 = 1.0 / sqrt(1.0 + m00 * m00);
+        m00 *= m01;
+      }
+      return {m01 * U.x - m00 * V.x, m01 * U.y - m00 * V.y, m01 * U.z - m00 * V.z};
+    }
+    return U;
+  }
+  if (fmax(a11, a01) > 0.0) {
+    if (a11 >= a01) {
+      m01 /= m11;
+      m11 = 1.0 / sqrt(1.0 + m01 * m01);
+      m01 *= m11;
+    } else {
+      m11 /= m01;
+      m01 = 1.0 / sqrt(1.0 + m11 * m11);
+      m11 *= m01;
+    }
+    return {m11 * U.x - m01 * V.x, m11 * U.y - m01 * V.y, m11 * U.z - m01 * V.z};
+  }
+  return U;
+}
+
+// FastEigen3x3: unit eigenvector of the smallest eigenvalue; 0 for C == 0.
+// (max over the 9 entries as Eigen's maxCoeff sees them: the symmetric pairs
+// are equal, so the 6 distinct ones.)
+__device__ V3 fast_eigen3x3(const S3& C) {
+  const double mx = fmax(fmax(fmax(C.a00, C.a01), fmax(C.a02, C.a11)), fmax(C.a12, C.a22));
+  if (mx == 0.0) return {0.0, 0.0, 0.0};
+  const S3 A{C.a00 / mx, C.a01 / mx, C.a02 / mx, C.a11 / mx, C.a12 / mx, C.a22 / mx};
+  const double norm = A.a01 * A.a01 + A.a02 * A.a02 + A.a12 * A.a12;
+  if (norm > 0.0) {
+    const double q = (A.a00 + A.a11 + A.a22) / 3.0;
+    const double b00 = A.a00 - q, b11 = A.a11 - q, b22 = A.a22 - q;
+    const double p = sqrt((b00 * b00 + b11 * b11 + b22 * b22 + norm * 2.0) / 6.0);
+    const double c00 = b11 * b22 - A.a12 * A.a12;
+    const double c01 = A.a01 * b22 - A.a12 * A.a02;
+    const double c02 = A.a01 * A.a12 - b11 * A.a02;
+    const double det = (b00 * c00 - A.a01 * c01 + A.a02 * c02) / (p * p * p);
+    const double half_det = fmin(fmax(det * 0.5, -1.0), 1.0);
+    const double angle = acos_det(half_det) / 3.0;
+    const double beta2 = cos_det(angle) * 2.0;
+    const double beta0 = cos_det(angle + 2.09439510239319549) * 2.0;
+    const double beta1 = -(beta0 + beta2);
+    const double ev0 = q + p * beta0, ev1 = q + p * beta1, ev2 = q + p * beta2;
+    if (half_det >= 0.0) {
+      const V3 e2 = evec0(A, ev2);
+      if (ev2 < ev0 && ev2 < ev1) return e2;
+      const V3 e1 = evec1(A, e2, ev1);
+      if (ev1 < ev0 && ev1 < ev2) return e1;
+      return cross(e1, e2);
+    }
+    const V3 e0 = evec0(A, ev0);
+    if (ev0 < ev1 && ev0 < ev2) return e0;
+    const V3 e1 = evec1(A, e0, ev1);
+    if (ev1 < ev0 && ev1 < ev2) return e1;
+    return cross(e0, e1);
+  }
+  if (C.a00 < C.a11 && C.a00 < C.a22) return {1.0, 0.0, 0.0};
+  if (C.a11 < C.a00 && C.a11 < C.a22) return {0.0, 1.0, 0.0};
+  return {0.0, 0.0, 1.0};
+}
+
+}  // namespace nrm
+
+constexpr int kNrmK = 32;  // largest max_nn
+
+// The 27 neighbour cells (-1: empty or outside) of every occupied cell of a
+// linear-key grid (key = (ix * ny + iy) * nz + iz), (dx, dy, dz) nesting order.
+__global__ __launch_bounds__(kT) void k_cell_neighbours_lin(const uint64_t* ukeys, int64_t m, int64_t nx, int64_t ny,
+                                                            int64_t nz, int32_t* nbr) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (c >= m) return;
+  const int64_t key = static_cast<int64_t>(ukeys[c]);
+  const int64_t x = key / (ny * nz), y = (key / nz) % ny, z = key % nz;
+  int e = 0;
+  for (int dx = -1; dx <= 1; ++dx)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dz = -1; dz <= 1; ++dz, ++e) {
+        const int64_t a = x + dx, b = y + dy, d = z + dz;
+        int64_t f = -1;
+        if (a >= 0 && a < nx && b >= 0 && b < ny && d >= 0 && d < nz)
+          f = find_cell(ukeys, m, static_cast<uint64_t>((a * ny + b) * nz + d));
+        nbr[27 * c + e] = static_cast<int32_t>(f);
+      }
+}
+
+// One query per thread, in cell-sorted order (neighbouring threads share
+// cells).  Candidates from the 27 cells of edge >= radius around the query's
+// cell; the max_nn best by (d2, index) in a sorted register list.
+__global__ __launch_bounds__(kT) void k_normals(const double* xyz, const double* sxyz, const uint32_t* sidx,
+                                                const uint64_t* skeys, int64_t n, const uint64_t* ukeys,
+                                                const uint32_t* ustart, int64_t m, const int32_t* nbr, double r2,
+                                                int max_nn, double* out) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (j >= n) return;
+  const double q0 = sxyz[3 * j], q1 = sxyz[3 * j + 1], q2 = sxyz[3 * j + 2];
+  const int64_t cell = find_cell(ukeys, m, skeys[j]);
+  double bd[kNrmK];
+  uint32_t bi[kNrmK];
+#pragma unroll
+  for (int e = 0; e < kNrmK; ++e) {
+    bd[e] = INFINITY;
+    bi[e] = 0xffffffffu;
+  }
+  int found = 0;
+  for (int e = 0; e < 27; ++e) {
+    const int32_t cc = nbr[27 * cell + e];
+    if (cc < 0) continue;
+    const int64_t t1 = cc + 1 < m ? static_cast<int64_t>(ustart[cc + 1]) : n;
+    for (int64_t t = ustart[cc]; t < t1; ++t) {
+      const double d0 = q0 - sxyz[3 * t], d1 = q1 - sxyz[3 * t + 1], d2 = q2 - sxyz[3 * t + 2];
+      const double dd = (d0 * d0 + d1 * d1) + d2 * d2;
+      if (!(dd < r2)) continue;
+      ++found;
+      const uint32_t id = sidx[t];
+      if (dd < bd[kNrmK - 1] || (dd == bd[kNrmK - 1] && id < bi[kNrmK - 1])) {
+        double v = dd;
+        uint32_t vi = id;
+#pragma unroll
+        for (int k = 0; k < kNrmK; ++k) {
+          const bool lt = v < bd[k] || (v == bd[k] && vi < bi[k]);
+          const double od = bd[k];
+          const uint32_t oi = bi[k];
+          bd[k] = lt ? v : od;
+          bi[k] = lt ? vi : oi;
+          v = lt ? od : v;
+          vi = lt ? oi : vi;
+        }
+      }
+    }
+  }
+  const int cnt = found < max_nn ? found : max_nn;
+  nrm::S3 C{1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
+  if (cnt >= 3) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0, s5 = 0.0, s6 = 0.0, s7 = 0.0, s8 = 0.0;
+#pragma unroll
+    for (int k = 0; k < kNrmK; ++k) {
+      if (k < cnt) {
+        const int64_t i = bi[k];
+        const double x = xyz[3 * i], y = xyz[3 * i + 1], z = xyz[3 * i + 2];
+        s0 += x;
+        s1 += y;
+        s2 += z;
+        s3 += x * x;
+        s4 += x * y;
+        s5 += x * z;
+        s6 += y * y;
+        s7 += y * z;
+        s8 += z * z;
+      }
+    }
+    const double k = static_cast<double>(cnt);
+    s0 /= k;
+    s1 /= k;
+    s2 /= k;
+    s3 /= k;
+    s4 /= k;
+    s5 /= k;
+    s6 /= k;
+    s7 /= k;
+    s8 /= k;
+    C = {s3 - s0 * s0, s4 - s0 * s1, s5 - s0 * s2, s6 - s1 * s1, s7 - s1 * s2, s8 - s2 * s2};
+  }
+  nrm::V3 v = nrm::fast_eigen3x3(C);
+  if (sqrt(v.x * v.x + v.y * v.y + v.z * v.z) == 0.0) v = {0.0, 0.0, 1.0};
+  const int64_t i = sidx[j];
+  out[3 * i] = v.x;
+  out[3 * i + 1] = v.y;
+  out[3 * i + 2] = v.z;
+}
+
+__global__ __launch_bounds__(kT) void k_fill_up(double* out, int64_t n) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i >= n) return;
+  out[3 * i] = 0.0;
+  out[3 * i + 1] = 0.0;
+  out[3 * i + 2] = 1.0;
+}
+
 // ------------------------------------------------------------------ host ----
 unsigned blocks(int64_t n) { return static_cast<unsigned>((n + kT - 1) / kT); }
 
@@ -1411,6 +1736,55 @@ int sl_transform_points(sl_ctx* c, double* xyz, int64_t n, const double* pose, v
   MTRY(c, hipSetDevice(slgpu_device(c)));
   hipLaunchKernelGGL(k_transform, dim3(blocks(n)), dim3(kT), 0, static_cast<hipStream_t>(stream), xyz, n, pose);
   MTRY(c, hipGetLastError());
+  return SL_OK;
+}
+
+// PointCloud::EstimateNormals(KDTreeSearchParamHybrid(radius, max_nn)) of a
+// cloud without normals (processing.py:178) -> normals [n, 3] f64.
+int sl_estimate_normals(sl_ctx* c, const double* xyz, int64_t n, double radius, int max_nn, double* normals,
+                        void* stream) {
+  if (!c || n < 0 || (n && (!xyz || !normals))) return SL_EINVAL;
+  if (max_nn > kNrmK) return slgpu_fail(c, SL_EINVAL, "max_nn > 32 is not supported");
+  if (std::isnan(radius)) return slgpu_fail(c, SL_EINVAL, "radius is NaN");
+  if (n >= (1ll << 31)) return slgpu_fail(c, SL_EINVAL, "at most 2^31 - 1 points");
+  if (n == 0) return SL_OK;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  PoolStream pool_stream(s);
+  MTRY(c, hipSetDevice(slgpu_device(c)));
+  // nanoflann searches radius * radius, so a negative radius acts as |radius|
+  const double r2 = radius * radius;
+  radius = fabs(radius);
+  if (!(r2 > 0.0) || max_nn < 3) {  // no point has 3 neighbours: identity covariance -> (0, 0, 1)
+    hipLaunchKernelGGL(k_fill_up, dim3(blocks(n)), dim3(kT), 0, s, normals, n);
+    MTRY(c, hipGetLastError());
+    return SL_OK;
+  }
+  double b[6];
+  int r = bounds(c, xyz, n, b, s);
+  if (r) return r;
+  double emax = 0.0;
+  for (int k = 0; k < 3; ++k) emax = std::max(emax, b[3 + k] - b[k]);
+  if (!std::isfinite(emax)) return slgpu_fail(c, SL_EINVAL, "non-finite point coordinates");
+  // cells of edge >= radius, so the 27 around a query's cell hold its ball;
+  // at most ~1e6 per axis
+  const double h = std::max(radius, emax / 1.0e6);
+  Grid g;
+  if (!make_grid(b, b + 3, h, &g)) return slgpu_fail(c, SL_EINVAL, "normal-search grid is too large");
+  DBuf<uint64_t> keys, ukeys;
+  DBuf<uint32_t> idx, ustart;
+  int64_t m = 0;
+  r = cells(c, xyz, n, g, keys, idx, ukeys, ustart, &m, s);
+  if (r) return r;
+  DBuf<double> sxyz;
+  DBuf<int32_t> nbr;
+  MTRY(c, sxyz.alloc(3 * n));
+  MTRY(c, nbr.alloc(27 * m));
+  hipLaunchKernelGGL(k_gather_sorted, dim3(blocks(n)), dim3(kT), 0, s, xyz, idx.p, n, sxyz.p);
+  hipLaunchKernelGGL(k_cell_neighbours_lin, dim3(blocks(m)), dim3(kT), 0, s, ukeys.p, m, g.nx, g.ny, g.nz, nbr.p);
+  hipLaunchKernelGGL(k_normals, dim3(blocks(n)), dim3(kT), 0, s, xyz, sxyz.p, idx.p, keys.p, n, ukeys.p, ustart.p, m,
+                     nbr.p, r2, max_nn, normals);
+  MTRY(c, hipGetLastError());
+  MTRY(c, hipStreamSynchronize(s));
   return SL_OK;
 }
 

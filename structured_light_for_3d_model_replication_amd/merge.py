@@ -8,8 +8,10 @@ with Open3D's arithmetic: same voxel grid, sums in point order, exact kNN, and
 sequential cloud statistics.  Voxel output is in ascending voxel key rather than
 Open3D's hash order.
 
-Open3D is not in this image, so parity is unpinned; oracle/merge_oracle.py is
-the restatement the tests check against.
+Then ``estimate_normals(KDTreeSearchParamHybrid(radius=2 voxel, max_nn=30))``
+(:178) and ``write_point_cloud`` (:181).  Open3D is not in this image, so
+parity is unpinned; oracle/merge_oracle.py is the restatement the tests check
+against.
 
 The reference aligns the views by FPFH + RANSAC + ICP (:145-157).  That
 registration is out of scope.  ``merge_pro_360_posed`` takes the poses instead:
@@ -123,6 +125,20 @@ def transform(points, pose, *, device=None) -> torch.Tensor:
     return P
 
 
+def estimate_normals(points, radius: float, max_nn: int = 30, *, device=None) -> torch.Tensor:
+    """PointCloud.estimate_normals(KDTreeSearchParamHybrid(radius, max_nn)) of a
+    cloud without normals (processing.py:178) -> normals f64 [N,3] on the
+    device (sl_estimate_normals; max_nn <= 32)."""
+    eng = _engine(device)
+    P = _f64(points, eng.device)
+    n = P.shape[0]
+    out = torch.empty((max(n, 1), 3), dtype=torch.float64, device=eng.device)
+    with eng._lock:
+        _lib.check(eng._L.sl_estimate_normals(eng._ctx, _ptr(P), n, float(radius), int(max_nn), out.data_ptr(),
+                                              eng._stream(None)), eng._ctx, "sl_estimate_normals")
+    return out[:n]
+
+
 def pool_trim(device=None) -> int:
     """Release the merge kernels' pooled scratch buffers of ``device``
     (sl_merge_pool_trim); returns the bytes released."""
@@ -162,8 +178,10 @@ def merge_pro_360_posed(input_folder, output_path, poses, voxel_size: float = 0.
     """merge_pro_360 (processing.py:116-182) with known per-file poses instead
     of the FPFH/RANSAC/ICP estimate: files in ``ply_files(order)`` order
     (default: the reference's lexicographic one), file i moved by ``poses[i]``
-    (4x4), merged, post-processed and written (binary PLY, Open3D's default;
-    ``binary=False`` for the ASCII format of sl_system.py)."""
+    (4x4), merged, post-processed, normals estimated (radius 2 voxel, max_nn 30,
+    :178) and written as o3d.io.write_point_cloud writes it (binary, double
+    xyz + normals, uchar RGB: ply.save_ply_open3d; ``binary=False``: the same
+    properties in ASCII).  Returns (points, colors, normals) on the device."""
     print(f"[Merge 360] Loading clouds from {input_folder}...")
     files = ply_files(input_folder, order)
     if len(files) < 2:
@@ -182,6 +200,7 @@ def merge_pro_360_posed(input_folder, output_path, poses, voxel_size: float = 0.
     merged_c = torch.cat(parts_c)
     print("[Merge 360] Post-processing (Downsample + Outlier removal)...")
     P, C = postprocess(merged_p, merged_c, voxel_size, device=eng.device)
-    ply.save_ply(P.cpu().numpy(), C.cpu().numpy(), output_path, binary=binary)
+    N = estimate_normals(P, voxel_size * 2, 30, device=eng.device)
+    ply.save_ply_open3d(P.cpu().numpy(), C.cpu().numpy(), output_path, normals=N.cpu().numpy(), binary=binary)
     print(f"[Merge 360] Saved merged cloud to {output_path}")
-    return P, C
+    return P, C, N

@@ -62,16 +62,58 @@ def save_ply(points, colors, filename, binary: bool = False) -> None:
                f"cannot write {filename}")
 
 
+def save_ply_open3d(points, colors, filename, normals=None, binary: bool = True) -> None:
+    """The file o3d.io.write_point_cloud writes for a cloud with points,
+    optional normals and colours (processing.py:181): binary little-endian
+    (``binary=False``: ASCII) with ``comment Created by Open3D``, double x y z,
+    double nx ny nz, uchar red green blue.  ``colors`` are BGR uint8 (written
+    as RGB).  Layout restated from Open3D's FilePLY.cpp; unpinned (no Open3D
+    in this image)."""
+    P = np.ascontiguousarray(np.asarray(points, dtype=np.float64)).reshape(-1, 3)
+    C = np.ascontiguousarray(np.asarray(colors, dtype=np.uint8)).reshape(-1, 3)
+    n = len(P)
+    if len(C) != n or (normals is not None and len(normals) != n):
+        raise ValueError("points, colors and normals differ in length")
+    fields = [("x", "<f8"), ("y", "<f8"), ("z", "<f8")]
+    if normals is not None:
+        fields += [("nx", "<f8"), ("ny", "<f8"), ("nz", "<f8")]
+    fields += [("red", "u1"), ("green", "u1"), ("blue", "u1")]
+    rec = np.empty(n, dtype=np.dtype(fields))
+    rec["x"], rec["y"], rec["z"] = P[:, 0], P[:, 1], P[:, 2]
+    if normals is not None:
+        Nn = np.asarray(normals, dtype=np.float64).reshape(-1, 3)
+        rec["nx"], rec["ny"], rec["nz"] = Nn[:, 0], Nn[:, 1], Nn[:, 2]
+    rec["red"], rec["green"], rec["blue"] = C[:, 2], C[:, 1], C[:, 0]
+    tnames = {"<f8": "double", "u1": "uchar"}
+    head = ["ply", f"format {'binary_little_endian' if binary else 'ascii'} 1.0", "comment Created by Open3D",
+            f"element vertex {n}"] + [f"property {tnames[t]} {nm}" for nm, t in fields] + ["end_header", ""]
+    with open(filename, "wb") as f:
+        f.write("\n".join(head).encode("ascii"))
+        if binary:
+            rec.tofile(f)
+        else:
+            # rply's ASCII writer: "%g" for doubles, "%d" for uchar, space-separated
+            cols = [rec[nm] for nm, _ in fields]
+            for i in range(n):
+                f.write((" ".join(f"{float(c[i]):g}" if c.dtype.kind == "f" else str(int(c[i])) for c in cols)
+                         + "\n").encode("ascii"))
+
+
 _PLY_TYPES = {"float": "<f4", "float32": "<f4", "double": "<f8", "float64": "<f8", "uchar": "u1",
               "uint8": "u1", "char": "i1", "int8": "i1", "short": "<i2", "int16": "<i2", "ushort": "<u2",
               "uint16": "<u2", "int": "<i4", "int32": "<i4", "uint": "<u4", "uint32": "<u4"}
 
 
-def read_ply(filename):
-    """-> (points float64 (N,3), colors uint8 (N,3) BGR) of a vertex-only PLY
-    (ASCII or binary_little_endian), as o3d.io.read_point_cloud feeds
-    processing.py:116-182.  Colour is swapped back to BGR, the reference's
-    in-memory order; a file without colour gives zeros."""
+def read_normals(filename):
+    """nx ny nz of a vertex-only PLY (float64 (N,3)), or None when absent."""
+    cols = _read_columns(filename)
+    if not all(c in cols for c in ("nx", "ny", "nz")):
+        return None
+    return np.stack([cols["nx"], cols["ny"], cols["nz"]], 1).astype(np.float64)
+
+
+def _read_columns(filename):
+    """{property: column} of a vertex-only PLY (ASCII or binary_little_endian)."""
     with open(filename, "rb") as f:
         data = f.read()
     end = data.find(b"end_header\n")
@@ -104,6 +146,16 @@ def read_ply(filename):
         cols = {p: rec[p] for p in names}
     else:
         raise ValueError(f"{filename}: unsupported format {fmt}")
+    return cols
+
+
+def read_ply(filename):
+    """-> (points float64 (N,3), colors uint8 (N,3) BGR) of a vertex-only PLY
+    (ASCII or binary_little_endian), as o3d.io.read_point_cloud feeds
+    processing.py:116-182.  Colour is swapped back to BGR, the reference's
+    in-memory order; a file without colour gives zeros."""
+    cols = _read_columns(filename)
+    n = len(cols["x"])
     P = np.stack([cols["x"], cols["y"], cols["z"]], 1).astype(np.float64)
     if all(c in cols for c in ("red", "green", "blue")):
         C = np.stack([cols["blue"], cols["green"], cols["red"]], 1).astype(np.uint8)

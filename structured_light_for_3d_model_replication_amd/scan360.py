@@ -14,7 +14,8 @@ default, f64 on request -- is gathered to rank 0 in view order over RCCL
 (``parallel.gather_cloud``: counts all-gathered, payloads point to point; or
 the C-ABI ``sl_gather`` with ``native_gather``).  Rank 0 optionally runs the
 merge post-processing of processing.py:171-175 (voxel downsample + statistical
-outlier removal, merge.py) and writes the merged PLY.
+outlier removal, merge.py), estimates the normals (:178) and writes the
+merged PLY in Open3D's layout.
 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
         -m structured_light_for_3d_model_replication_amd.scan360 SCAN_DIR calib.mat \\
@@ -115,12 +116,16 @@ def scan_distributed(parent_dir, calib_data, *, poses=None, n_cols=1920, n_rows=
         P, C, counts = parallel.gather_cloud(xyz, bgr, dst=0, group=group)
     if rank != 0:
         return None, None, counts
+    N = None
     if voxel_size:
         from . import merge
         P, C = merge.postprocess(P, C, voxel_size, nb_neighbors, std_ratio, device=P.device)
+        if merge_output:  # processing.py:178
+            N = merge.estimate_normals(P, voxel_size * 2, 30, device=P.device)
     if merge_output:
         from . import ply
-        ply.save_ply(P.cpu().numpy(), C.cpu().numpy(), merge_output, binary=True)
+        ply.save_ply_open3d(P.cpu().numpy(), C.cpu().numpy(), merge_output,
+                            normals=None if N is None else N.cpu().numpy())
         log(f"[scan360] merged {sum(counts)} points from {len(views)} views on {world} GPU(s) -> "
             f"{len(P)} points, {merge_output}")
     return P, C, counts

@@ -57,3 +57,51 @@ def test_statistical_edge_cases():
     # a single point: std over n - 1 = 0 points is nan -> nothing kept
     ind, _ = mo.remove_statistical_outlier(np.array([[1.0, 2.0, 3.0]]), 20, 2.0)
     assert len(ind) == 0
+
+
+def test_det_math_within_one_ulp():
+    """The fdlibm acos / cos both normal paths use (oracle and slmerge.hip)
+    stay within 1 ulp of the exact value on FastEigen3x3's ranges (acos on
+    [-1, 1], cos on [0, pi/3] and [2pi/3, pi])."""
+    import mpmath
+    mpmath.mp.prec = 120
+    rng = np.random.default_rng(3)
+    xs = np.concatenate([rng.uniform(-1, 1, 400), [-1.0, 1.0, 0.5, -0.5, 0.0, 1 - 2**-53, -1 + 2**-53]])
+    for x in xs:
+        e = float(mpmath.acos(mpmath.mpf(float(x))))
+        assert abs(mo.acos_det(float(x)) - e) <= np.spacing(abs(e)) if e else mo.acos_det(float(x)) == 0.0
+    ys = np.concatenate([rng.uniform(0, np.pi / 3, 300), rng.uniform(2 * np.pi / 3, np.pi, 300),
+                         [0.0, np.pi / 3, 2.09439510239319549, np.pi]])
+    for y in ys:
+        e = float(mpmath.cos(mpmath.mpf(float(y))))
+        assert abs(mo.cos_det(float(y)) - e) <= np.spacing(abs(e))
+
+
+def test_normals_oracle_is_the_smallest_eigenvector():
+    """estimate_normals' FastEigen3x3 vs numpy's eigh of the same neighbour
+    covariance: the same direction (|cos| = 1 within 1e-12) wherever the
+    smallest eigenvalue is well separated; unit length everywhere."""
+    rng = np.random.default_rng(4)
+    u = rng.normal(size=(1500, 3))
+    P = 50.0 * u / np.linalg.norm(u, axis=1, keepdims=True) + rng.normal(0, 0.3, (1500, 3))
+    N = mo.estimate_normals(P, 9.0, 30)
+    np.testing.assert_allclose(np.linalg.norm(N, axis=1), 1.0, rtol=1e-12)
+    checked = 0
+    for i, nb in enumerate(mo.hybrid_neighbours(P, 9.0, 30)):
+        if len(nb) < 3:
+            continue
+        w, v = np.linalg.eigh(np.cov(P[nb].T, bias=True))
+        if w[1] - w[0] > 1e-6 * w[2]:
+            assert abs(abs(v[:, 0] @ N[i]) - 1.0) < 1e-9
+            checked += 1
+    assert checked > 1000
+
+
+def test_normals_oracle_degenerate_cases():
+    # fewer than 3 neighbours -> identity covariance -> (0, 0, 1); a plane -> +-z
+    np.testing.assert_array_equal(mo.estimate_normals(np.array([[0.0, 0, 0], [1.0, 0, 0]]), 0.5),
+                                  [[0, 0, 1.0], [0, 0, 1.0]])
+    g = np.arange(6, dtype=float)
+    plane = np.stack(np.meshgrid(g, g, [0.0], indexing="ij"), -1).reshape(-1, 3)
+    N = mo.estimate_normals(plane, 1.5, 30)
+    np.testing.assert_array_equal(np.abs(N), np.tile([0.0, 0.0, 1.0], (len(plane), 1)))

@@ -144,3 +144,31 @@ def test_merge_file_orders(tmp_path):
     assert num == ["view_0deg.ply", "zz.PLY", "view_10deg.ply", "view_20deg.ply", "view_100deg.ply"]
     with pytest.raises(ValueError):
         merge.ply_files(str(tmp_path), "mtime")
+
+
+@pytest.mark.parametrize("binary", [True, False])
+def test_open3d_layout_writer_round_trip(tmp_path, binary):
+    """save_ply_open3d: the layout o3d.io.write_point_cloud writes for points +
+    normals + colours (double x y z nx ny nz, uchar RGB); read back exactly
+    (binary) / to %g (ASCII)."""
+    rng = np.random.default_rng(2)
+    P = rng.normal(size=(50, 3)) * 100
+    N = rng.normal(size=(50, 3))
+    C = rng.integers(0, 256, (50, 3), dtype=np.uint8)
+    f = str(tmp_path / "o3d.ply")
+    ply.save_ply_open3d(P, C, f, normals=N, binary=binary)
+    head = open(f, "rb").read().split(b"end_header\n")[0].decode()
+    assert "comment Created by Open3D" in head
+    assert [ln.split()[-1] for ln in head.splitlines() if ln.startswith("property")] == \
+        ["x", "y", "z", "nx", "ny", "nz", "red", "green", "blue"]
+    P2, C2 = ply.read_ply(f)
+    N2 = ply.read_normals(f)
+    np.testing.assert_array_equal(C2, C)
+    if binary:
+        np.testing.assert_array_equal(P2, P)
+        np.testing.assert_array_equal(N2, N)
+    else:
+        np.testing.assert_allclose(P2, P, rtol=1e-5)
+        np.testing.assert_allclose(N2, N, rtol=1e-5, atol=1e-5)
+    ply.save_ply_open3d(P, C, f)
+    assert ply.read_normals(f) is None

@@ -134,9 +134,10 @@ def test_scan_distributed_gpu_world1(tmp_path):
         Pe, Ce = merge.postprocess(P, C, 5.0)
         np.testing.assert_array_equal(Pm.cpu().numpy(), Pe.cpu().numpy())
         np.testing.assert_array_equal(Cm.cpu().numpy(), Ce.cpu().numpy())
-        Pr, Cr = ply.read_ply(out)  # binary PLY: float32 xyz
-        np.testing.assert_array_equal(np.asarray(Pr, np.float32), Pm.cpu().numpy().astype(np.float32))
+        Pr, Cr = ply.read_ply(out)  # Open3D layout: double xyz + normals
+        np.testing.assert_array_equal(Pr, Pm.cpu().numpy())
         np.testing.assert_array_equal(np.asarray(Cr), Cm.cpu().numpy())
+        np.testing.assert_array_equal(ply.read_normals(out), merge.estimate_normals(Pm, 10.0).cpu().numpy())
     finally:
         dist.destroy_process_group()
 
