@@ -5,7 +5,14 @@ Mirrors the file handling of gray_decode (server/sl_system.py:510-520, 556-557,
 8-bit gray (``cv2.imread(f, 0)``) and file 0 re-read in colour (BGR) for the
 texture.
 
-OpenCV is not available in this image, so decoding uses Pillow.  For
+Uncompressed BMP files (the capture format the GUI saves, sl_system.py:519)
+are read by ``read_bmp_gray`` straight from the file's pixel array: header
+parse, then one strided copy of the rows (bottom-up rows flipped, the 4-byte
+row padding dropped) -- checked byte for byte against Pillow's decoder in
+tests/test_ingest.py.  Anything else (PNG, JPEG bytes under a .bmp name, RLE
+BMPs) goes through Pillow.
+
+OpenCV is not available in this image, so the other decoding uses Pillow.  For
 single-channel files (what the fixtures and the synthetic rig produce) gray is
 the identity and colour is the channel replicated three times, exactly what
 cv2 returns.  Colour files are converted with OpenCV's fixed-point BT.601
@@ -37,8 +44,84 @@ def _rgb_to_gray_cv(rgb: np.ndarray) -> np.ndarray:
     return ((1868 * b + 9617 * g + 4899 * r + 8192) >> 14).astype(np.uint8)
 
 
-def imread_gray(path: str) -> np.ndarray:
+_BMP_INFO = (40, 52, 56, 108, 124)  # BITMAPINFOHEADER and its V2..V5 extensions
+
+
+def _bmp_layout(head: bytes):
+    """(offset, H, W, bpp, bottom_up, palette_bgr | None) of an uncompressed
+    8/24/32-bit BMP, from its first bytes, or None when the raw path does not
+    apply (not 'BM', RLE / bitfield compression, other depths)."""
+    if len(head) < 54 or head[:2] != b"BM":
+        return None
+    off = int.from_bytes(head[10:14], "little")
+    dib = int.from_bytes(head[14:18], "little")
+    if dib not in _BMP_INFO:
+        return None
+    W = int.from_bytes(head[18:22], "little", signed=True)
+    H = int.from_bytes(head[22:26], "little", signed=True)
+    planes = int.from_bytes(head[26:28], "little")
+    bpp = int.from_bytes(head[28:30], "little")
+    comp = int.from_bytes(head[30:34], "little")
+    if planes != 1 or W <= 0 or H == 0 or bpp not in (8, 24, 32):
+        return None
+    if comp != 0 and not (comp == 3 and bpp == 32 and dib >= 52 and
+                          head[54:66] == bytes.fromhex("0000ff0000ff0000ff000000")):
+        return None  # BI_RGB, or BI_BITFIELDS with the default BGRx masks only
+    pal = None
+    if bpp == 8:
+        n = int.from_bytes(head[46:50], "little") or 256
+        p0 = 14 + dib
+        if len(head) < p0 + 4 * n:
+            return None
+        pal = np.frombuffer(head, np.uint8, 4 * n, p0).reshape(n, 4)[:, :3]
+    return off, abs(H), W, bpp, H > 0, pal
+
+
+def read_bmp_gray(path: str, out: np.ndarray | None = None) -> np.ndarray | None:
+    """cv2.imread(path, 0) of an uncompressed BMP without a full decode:
+    8-bit (palette mapped; gray palettes are the identity), 24/32-bit BGR(x)
+    through OpenCV's fixed-point gray weights.  Writes into ``out`` (uint8
+    [H, W]) when given.  None when the file is not such a BMP (the caller
+    then decodes it with Pillow)."""
+    with open(path, "rb") as f:
+        head = f.read(14 + 124 + 1024)  # file header, largest info header, 256-entry palette
+        lay = _bmp_layout(head)
+        if lay is None:
+            return None
+        off, H, W, bpp, bottom_up, pal = lay
+        bpr = W * bpp // 8
+        stride = (bpr + 3) & ~3
+        f.seek(off)
+        raw = f.read(stride * H)
+    if len(raw) < stride * H - (stride - bpr):
+        raise ValueError(f"{path}: truncated BMP pixel array")
+    raw = raw.ljust(stride * H, b"\0")
+    rows = np.frombuffer(raw, np.uint8).reshape(H, stride)[:, :bpr]
+    if bottom_up:
+        rows = rows[::-1]
+    if out is None:
+        out = np.empty((H, W), np.uint8)
+    elif out.shape != (H, W):
+        raise ValueError(f"{path}: size {(H, W)} differs from {tuple(out.shape)}")
+    if bpp == 8:
+        gray = pal[:, 0] if np.all(pal == pal[:, :1]) else _rgb_to_gray_cv(pal[:, ::-1])
+        if len(gray) == 256 and np.array_equal(gray, np.arange(256, dtype=np.uint8)):
+            out[...] = rows
+        else:
+            lut = np.zeros(256, np.uint8)
+            lut[: len(gray)] = gray[:256]
+            np.take(lut, rows, out=out)
+    else:
+        px = rows.reshape(H, W, bpp // 8)
+        out[...] = _rgb_to_gray_cv(px[:, :, 2::-1])
+    return out
+
+
+def imread_gray(path: str, out: np.ndarray | None = None) -> np.ndarray:
     """cv2.imread(path, 0) equivalent (uint8 H x W)."""
+    a = read_bmp_gray(path, out)
+    if a is not None:
+        return a
     with Image.open(path) as im:
         if im.mode == "L":
             return np.asarray(im).copy()
@@ -62,17 +145,17 @@ def frame_size(path: str) -> tuple[int, int]:
         return im.size[1], im.size[0]
 
 
-_POOL = None
+_POOLS: dict = {}
 _POOL_LOCK = threading.Lock()
 
 
 def _pool(workers: int):
-    global _POOL
+    """A persistent pool of exactly ``workers`` decoding threads."""
     from concurrent.futures import ThreadPoolExecutor
     with _POOL_LOCK:
-        if _POOL is None or _POOL._max_workers < workers:
-            _POOL = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="sl-ingest")
-        return _POOL
+        if workers not in _POOLS:
+            _POOLS[workers] = ThreadPoolExecutor(max_workers=workers, thread_name_prefix="sl-ingest")
+        return _POOLS[workers]
 
 
 def fill_stack(files: list[str], stack_out, tex_out, workers: int = 8) -> bool:
@@ -87,10 +170,12 @@ def fill_stack(files: list[str], stack_out, tex_out, workers: int = 8) -> bool:
     shape = tuple(stack_out.shape[1:])
 
     def one(j):
-        a = imread_gray(files[j])
-        if a.shape != shape:
-            raise ValueError(f"{files[j]}: size {a.shape} differs from {shape}")
-        stack_out[j] = a
+        dst = stack_out[j]
+        a = imread_gray(files[j], dst)  # an uncompressed BMP is read straight into dst
+        if a is not dst:
+            if a.shape != shape:
+                raise ValueError(f"{files[j]}: size {a.shape} differs from {shape}")
+            dst[...] = a
 
     if workers > 1 and n > 1:
         list(_pool(workers).map(one, range(n)))
