@@ -2,14 +2,74 @@
 
     python -m structured_light_for_3d_model_replication_amd.process_cloud --input scan/ --output out.ply
 
-Same flags, defaults and behaviour (Old/process_cloud.py:221-236): errors are
-printed, not raised.  Uses the fixed-threshold mask of that file (:47-49).
+Same flags, defaults, prints and behaviour as Old/process_cloud.py:221-236:
+``load_calibration`` announces the file (:12), ``gray_decode`` warns when
+fewer than 2 (n_col_bits + n_row_bits) pattern files are present (:56-58) and
+uses that file's fixed-threshold mask (:47-49), every step prints its line,
+and errors are printed as ``Error: ...``, not raised.  The stdout and the PLY
+bytes are pinned by tests/golden/cli_process_cloud.npz, made by running the
+reference CLI's own functions.  Decoding and triangulation run on the GPU
+(libslgpu.so).
 """
 from __future__ import annotations
 
 import argparse
+import os
 
-from .multi_point_cloud_process import gray_decode, load_calibration, reconstruct_point_cloud, save_ply
+import numpy as np
+import scipy.io
+import torch
+
+from . import core, io, ply
+from .pipeline import bit_count
+from .sl_system import reconstruct_point_cloud
+
+
+def load_calibration(calib_path):
+    """Old/process_cloud.py:8-23."""
+    if not os.path.exists(calib_path):
+        raise FileNotFoundError(f"Calibration file not found at {calib_path}")
+    print(f"Loading calibration from {calib_path}...")
+    data = scipy.io.loadmat(calib_path)
+    return {"Nc": data["Nc"], "Oc": data["Oc"], "wPlaneCol": data["wPlaneCol"], "wPlaneRow": data["wPlaneRow"],
+            "cam_K": data["cam_K"]}
+
+
+def gray_decode(folder, n_cols=1920, n_rows=1080, *, device=None):
+    """Old/process_cloud.py:25-106 (fixed mask white > 40, white - black > 10).
+
+    The reference reads the pattern pairs as it decodes, so a dangling odd
+    file raises IndexError inside the column or the row loop (after the
+    matching "Decoding ..." line); the stack is checked here up front and the
+    same lines are printed before the same error."""
+    files = io.list_stack_files(folder)
+    if len(files) < 4:
+        raise ValueError("Not enough images in folder to decode.")
+    nc, nr = bit_count(n_cols), bit_count(n_rows)
+    total = (nc + nr) * 2
+    if len(files) - 2 < total:
+        print(f"Warning: Expected {total} pattern files, found {len(files) - 2}")
+    pairs = (len(files) - 2) // 2
+    dangling = (len(files) - 2) % 2 == 1 and pairs < nc + nr
+    print("Decoding Columns...")
+    if dangling and pairs < nc:
+        raise IndexError("list index out of range")
+    print("Decoding Rows...")
+    if dangling:
+        raise IndexError("list index out of range")
+    stack, texture, _ = io.read_stack(folder)
+    eng = core.engine(device)
+    res = eng.decode_triangulate(torch.from_numpy(stack).to(eng.device), n_cols, n_rows, mask_mode="fixed",
+                                 maps=True, cloud=False)
+    eng.sync()
+    return (res["col_map"][0].cpu().numpy(), res["row_map"][0].cpu().numpy(), res["mask"][0].cpu().numpy(),
+            texture)
+
+
+def save_ply(points, colors, filename):
+    """Old/process_cloud.py:199-219."""
+    print(f"Saving {len(points)} points to {filename}...")
+    ply.save_ply(np.asarray(points), np.asarray(colors), filename)
 
 
 def main(argv=None):

@@ -78,7 +78,14 @@ def load_reference():
     tree2 = ast.parse(open(p2, encoding="utf-8").read())
     want = {"load_calibration", "gray_decode", "reconstruct_point_cloud", "save_ply"}
     mp = _compile_defs(p2, [n for n in tree2.body if isinstance(n, ast.FunctionDef) and n.name in want])
+    p3 = os.path.join(REF, "Old", "process_cloud.py")
+    tree3 = ast.parse(open(p3, encoding="utf-8").read())
+    cli = _compile_defs(p3, [n for n in tree3.body if isinstance(n, ast.FunctionDef) and n.name in want])
     return {
+        "cli_load_calibration": cli["load_calibration"],
+        "cli_gray_decode": cli["gray_decode"],
+        "cli_reconstruct": cli["reconstruct_point_cloud"],
+        "cli_save_ply": cli["save_ply"],
         "sl_gray_decode": sl["gray_decode"],
         "sl_reconstruct": sl["reconstruct_point_cloud"],
         "sl_generate_cloud": sl["generate_cloud"],
@@ -135,9 +142,53 @@ def nonzero_oc_case(ref, tmp):
               stack=st, texture=tex, col_map=col, row_map=row, mask=mask, P=P, C=C, **calib_arrays(cal))
 
 
+def cli_cases(ref, tmp):
+    """Old/process_cloud.py's CLI: its __main__ sequence (:221-236) --
+    load_calibration, gray_decode (fixed mask, the "Warning: Expected N
+    pattern files" print), reconstruct_point_cloud, save_ply, "Done!" / the
+    printed error -- run on a full stack, a short stack (warning, fewer bits),
+    an odd file count (IndexError) and a missing calib file.  Stored: the
+    stdout (folder paths as {DIR}) and the PLY text."""
+    import contextlib
+    import io as _io
+    rig, st, _ = render(40, 56, 1920, 1080, seed=24)
+    cal = synth.make_calibration(rig)
+    mat = os.path.join(tmp, "cli_calib.mat")
+    scipy.io.savemat(mat, cal)
+    cases = {"full": st, "short": st[:12], "odd": st[:9], "nocalib": st}
+    meta = {}
+    arrays = {"stack": st, **calib_arrays(cal)}
+    for name, stack in cases.items():
+        folder = os.path.join(tmp, f"cli_{name}")
+        write_stack(folder, stack, ext=".bmp")
+        out = os.path.join(tmp, f"cli_{name}.ply")
+        buf = _io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            try:  # the __main__ block of Old/process_cloud.py, with its arguments
+                calib_data = ref["cli_load_calibration"](mat if name != "nocalib" else mat + ".missing")
+                c_map, r_map, mask, texture = ref["cli_gray_decode"](folder)
+                points, colors = ref["cli_reconstruct"](c_map, r_map, mask, texture, calib_data)
+                ref["cli_save_ply"](points, colors, out)
+                print("Done!")
+            except Exception as e:  # noqa: BLE001 -- the reference prints every error
+                print(f"Error: {e}")
+        meta[name] = {"files": int(len(stack)), "stdout": buf.getvalue().replace(tmp, "{DIR}")}
+        if os.path.exists(out):
+            shutil.copy(out, os.path.join(HERE, f"cli_process_cloud_{name}.ply"))
+            meta[name]["ply"] = f"cli_process_cloud_{name}.ply"
+    save_case("cli_process_cloud", {"func": "cli", "cases": meta}, **arrays)
+    print("cli:", {k: v["stdout"].splitlines()[-1] for k, v in meta.items()})
+
+
 def main():
     ref = load_reference()
     tmp = tempfile.mkdtemp(prefix="golden_")
+    if "--only-cli" in sys.argv:
+        try:
+            cli_cases(ref, tmp)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     if "--only-nonzero-oc" in sys.argv:  # add the one case without rewriting the others
         try:
             nonzero_oc_case(ref, tmp)
@@ -302,6 +353,7 @@ def main():
         save_case("errors", {"errors": errs, "n_cols": 16, "n_rows": 8}, stack=st)
         print("errors:", errs)
         nonzero_oc_case(ref, tmp)
+        cli_cases(ref, tmp)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
