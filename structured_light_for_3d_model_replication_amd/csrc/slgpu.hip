@@ -42,6 +42,7 @@
 #include <cmath>
 #include <initializer_list>
 #include <string>
+#include <type_traits>
 #include <thread>
 #include <vector>
 
@@ -1152,6 +1153,35 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
                                              int total, const uint32_t* s_ent, const uint32_t* s_bgr,
                                              float* s_sxyz, uint8_t* s_scol);
 
+// base + a 32-bit byte offset: the form global loads / stores take with an
+// SGPR base (wave-uniform pointer) and a 32-bit VGPR offset
+template <typename T>
+__device__ __forceinline__ T* at_bytes(T* base, unsigned off) {
+  using B = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  return reinterpret_cast<T*>(reinterpret_cast<B*>(base) + off);
+}
+
+// Pixel (u, v) of chunk-local pixel `local` (the chunk starts at (u_c, v_c)):
+// one row wrap at most when W >= kChunk (wave-uniform test), else a loop.
+// The range facts let the table gathers use 32-bit offsets.
+__device__ __forceinline__ void chunk_uv(int u_c, int v_c, int local, int W, int* u, int* v) {
+  int uu = u_c + local, vv = v_c;
+  if (W >= kChunk) {
+    const bool wrap = uu >= W;
+    uu -= wrap ? W : 0;
+    vv += wrap ? 1 : 0;
+  } else {
+    while (uu >= W) {
+      uu -= W;
+      ++vv;
+    }
+  }
+  __builtin_assume(uu >= 0 && uu < (1 << 24));
+  __builtin_assume(vv >= 0 && vv < (1 << 24));
+  *u = uu;
+  *v = vv;
+}
+
 // One chunk (global index gc, output offset base) of k_cloud, by one wave.
 template <int MODE, int VEC>
 __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane,
@@ -1289,6 +1319,8 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
     }
     return static_cast<uint32_t>(p.stack[view * p.stack_vs + cpx + local]) * 0x010101u;
   };
+  float* const wx = static_cast<float*>(p.xyz) + 3 * base;  // the chunk's first point (wave-uniform)
+  uint8_t* const wc = p.bgr + 3 * base;
   for (int j0 = 0; j0 < total; j0 += 64 * kPipe) {
     if (mode & M_FAST32) {
       // SL_XYZ_F32_FAST (Oc = 0, pinhole rays, no pose; host-checked): the
@@ -1306,13 +1338,16 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         const uint32_t e = s_ent[j];
         const int local = static_cast<int>(e & 1023u);
         bgr[i] = point_bgr(j, local);
-        int uu = u_c + local, vv = v_c;
-        while (uu >= W) {
-          uu -= W;
-          ++vv;
+        int uu, vv;
+        chunk_uv(u_c, v_c, local, W, &uu, &vv);
+        if (kAblate & 512) {  // measurement only: no table gathers
+          fx[i] = 0.001f * static_cast<float>(uu);
+          fy[i] = 0.001f * static_cast<float>(vv);
+          fp[i] = make_float4(0.1f, 0.2f, 0.9f, -500.0f - static_cast<float>(e >> 10));
+          continue;
         }
-        fx[i] = p.xn32[static_cast<unsigned>(uu)];
-        fy[i] = p.yn32[static_cast<unsigned>(vv)];
+        fx[i] = *at_bytes(p.xn32, 4u * static_cast<unsigned>(uu));
+        fy[i] = *at_bytes(p.yn32, 4u * static_cast<unsigned>(vv));
         fp[i] = p.planes32[e >> 10];
       }
 #pragma unroll
@@ -1332,11 +1367,8 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           Z = 0.0f + inv * t;
         } else {  // ill-conditioned: exact f64, as the path below
           const uint32_t e = s_ent[min(j, total - 1)];
-          int uu = u_c + static_cast<int>(e & 1023u), vv = v_c;
-          while (uu >= W) {
-            uu -= W;
-            ++vv;
-          }
+          int uu, vv;
+          chunk_uv(u_c, v_c, static_cast<int>(e & 1023u), W, &uu, &vv);
           const double xd = p.xn[uu], yd = p.yn[vv];
           const double4 pd = p.planes[e >> 10];
           const double nrm = sqrt((xd * xd + yd * yd) + 1.0);
@@ -1346,12 +1378,14 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           Y = static_cast<float>(p.o1 + d1 * td);
           Z = static_cast<float>(p.o2 + d2 * td);
         }
-        if (j < total) {
-          float* xyz = static_cast<float*>(p.xyz) + 3 * base + 3 * static_cast<unsigned>(j);
+        if (kAblate & 256) {  // measurement only: no point stores (results kept live)
+          if (X == -1234.5f && Y == Z) p.bgr[0] = static_cast<uint8_t>(bgr[i]);
+        } else if (j < total) {
+          float* xyz = at_bytes(wx, 12u * static_cast<unsigned>(j));
           xyz[0] = X;
           xyz[1] = Y;
           xyz[2] = Z;
-          uint8_t* cc = p.bgr + 3 * base + 3 * static_cast<unsigned>(j);
+          uint8_t* cc = at_bytes(wc, 3u * static_cast<unsigned>(j));
           cc[0] = static_cast<uint8_t>(bgr[i]);
           cc[1] = static_cast<uint8_t>(bgr[i] >> 8);
           cc[2] = static_cast<uint8_t>(bgr[i] >> 16);
@@ -1382,13 +1416,10 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         rb[i] = p.nc_rays[HW + q];
         rcz[i] = p.nc_rays[2 * HW + q];
       } else {
-        int uu = u_c + local, vv = v_c;
-        while (uu >= W) {
-          uu -= W;
-          ++vv;
-        }
-        ra[i] = p.xn[static_cast<unsigned>(uu)];
-        rb[i] = p.yn[static_cast<unsigned>(vv)];
+        int uu, vv;
+        chunk_uv(u_c, v_c, local, W, &uu, &vv);
+        ra[i] = p.xn[uu];
+        rb[i] = p.yn[vv];
       }
       pl[i] = p.planes[c];
     }
@@ -1468,12 +1499,12 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           xyz[1] = Y[i];
           xyz[2] = Z[i];
         } else {
-          float* xyz = static_cast<float*>(p.xyz) + 3 * base + 3 * o;
+          float* xyz = at_bytes(wx, 12u * o);
           xyz[0] = static_cast<float>(X[i]);
           xyz[1] = static_cast<float>(Y[i]);
           xyz[2] = static_cast<float>(Z[i]);
         }
-        uint8_t* cc = p.bgr + 3 * base + 3 * o;
+        uint8_t* cc = at_bytes(wc, 3u * o);
         cc[0] = static_cast<uint8_t>(bgr[i]);
         cc[1] = static_cast<uint8_t>(bgr[i] >> 8);
         cc[2] = static_cast<uint8_t>(bgr[i] >> 16);
