@@ -188,6 +188,7 @@ struct Params {
   const int64_t* base_in;  // points of the earlier launch groups of this call, or null
   int* chunk_counts;       // k_count -> k_cloud: points per chunk
   int* block_sums;         // k_count -> k_cloud: points per workgroup (4 chunks)
+  int bs_atomic;           // k_decode M_DECIDE: block sums by the last wave to arrive (no barrier)
 };
 
 // ---------------------------------------------------------------- helpers ----
@@ -460,6 +461,7 @@ __device__ __forceinline__ uint32_t mask4(uint32_t w, uint32_t b, uint32_t tw2, 
 #endif
 constexpr bool kDecYnLds = SLGPU_DEC_YN_LDS != 0;  // yn in LDS (else one early global load per lane)
 constexpr int kDecPl = 2048, kDecX = 4096, kDecY = 4096;
+constexpr int kBsSlots = 16;  // k_decode M_DECIDE: chunk-group iterations per workgroup with a barrier-free block sum
 constexpr int kDecodeLds = (kDecPl * 4 + kDecX + (kDecYnLds ? kDecY : 0)) * 4;  // bytes: > the histogram replicas
 static_assert(kDecodeLds >= 256 * kHistStride * 4, "the decode LDS holds the histogram replicas too");
 
@@ -498,6 +500,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   __shared__ __attribute__((aligned(16))) unsigned s_lds[kDecodeLds / 4];
   __shared__ int s_max[kWaves];
   __shared__ int s_cnt[2][kWaves];
+  __shared__ unsigned s_bsum[kBsSlots];  // per iteration: points (low 16 bits) + waves arrived << 16
   unsigned* s_hist = s_lds;
   float4* s_pl = reinterpret_cast<float4*>(s_lds);
   float* s_xn = reinterpret_cast<float*>(s_lds) + 4 * kDecPl;
@@ -509,6 +512,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   const int view = blockIdx.y;
   const int64_t HW = p.HW;
   if (decide) {
+    if (tid < kBsSlots) s_bsum[tid] = 0u;
     for (int i = tid; i < p.Wp; i += kThreads) s_pl[i] = p.planes32[i];
     for (int i = tid; i < p.W; i += kThreads) s_xn[i] = p.xn32[i];
     if (kDecYnLds)
@@ -761,7 +765,16 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         const int cnt = wave_sum(__popc(pt));
         if (lane == 0) {
           if (live) p.chunk_counts[gci] = cnt;
-          s_cnt[it & 1][wid] = live ? cnt : 0;
+          const unsigned mine = live ? static_cast<unsigned>(cnt) : 0u;
+          if (p.bs_atomic) {
+            // the workgroup's block sum without a barrier: the last of its
+            // waves to add its count (one LDS slot per iteration) writes it
+            const unsigned old = atomicAdd(&s_bsum[it], (1u << 16) | mine);
+            if ((old >> 16) == kWaves - 1)
+              p.block_sums[static_cast<int64_t>(view) * ngroups + cg] = static_cast<int>((old & 0xffffu) + mine);
+          } else {
+            s_cnt[it & 1][wid] = static_cast<int>(mine);
+          }
         }
       }
     }
@@ -799,7 +812,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         if (k < n_px) p.codes[o + k] = static_cast<uint16_t>(rec[k >> 1] >> (16 * (k & 1)));
     }
   }
-  if (decide && (mode & M_CODES)) {  // the workgroup's block sum (k_count's, for k_cloud's offsets)
+  if (decide && (mode & M_CODES) && !p.bs_atomic) {  // the workgroup's block sum (k_count's, for k_cloud's offsets)
     __syncthreads();
     if (tid == 0) {
       int t = 0;
@@ -1826,6 +1839,9 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     dim3 dgrid = grid;  // k_decode: chunk groups strided over a capped grid
     if (c->decode_wgs > 0) dgrid.x = std::min(grid.x, static_cast<unsigned>(std::max(1, (c->decode_wgs + nv - 1) / nv)));
     c->last.grid[0] = dgrid;
+    // barrier-free block sums when every k_decode workgroup iterates at most
+    // kBsSlots chunk groups (4 chunks of at most 1024 points: 16-bit sums)
+    p.bs_atomic = decide && (grid.x + dgrid.x - 1) / dgrid.x <= static_cast<unsigned>(kBsSlots);
     c->last.grid[1] = c->last.grid[2] = grid;
     c->last.s = s;
     c->last.fn[2] = nullptr;
