@@ -5,10 +5,10 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/bsa
 mkdir -p $O
-SLGPU_LIB=$PWD/build/libslgpu_bsa.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+SLGPU_LIB=$PWD/build/libslgpu_late.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 : > $O/kb.log
-for v in default bsa; do
+for v in early late; do
   lib=structured_light_for_3d_model_replication_amd/libslgpu.so
   [ $v != default ] && lib=build/libslgpu_$v.so
   for args in "--fast --only maps+cloud" "--fast --only cloud" "--fast --only cloud --views 8 --H 1080 --W 1920" "--fast --only cloud --views 4 --H 3000 --W 4000" "--fast --only maps+cloud --H 720 --W 1280"; do
