@@ -135,7 +135,7 @@ constexpr int kHistStride = kHistRep + 1;  // bin stride: replica r of bin b sit
 constexpr int kAblate = SLGPU_ABLATE;
 constexpr int kMaxWp = 32768;              // projector columns (record codes are 15 bits)
 #ifndef SLGPU_MAX_CHUNKS
-#define SLGPU_MAX_CHUNKS (1 << 14)
+#define SLGPU_MAX_CHUNKS (1 << 16)
 #endif
 constexpr int64_t kMaxChunks = SLGPU_MAX_CHUNKS;  // chunks per launch group: bounds k_cloud's prefix reads
 
@@ -189,6 +189,13 @@ struct Params {
   int* chunk_counts;       // k_count -> k_cloud: points per chunk
   int* block_sums;         // k_count -> k_cloud: points per workgroup (4 chunks)
   int bs_atomic;           // k_decode M_DECIDE: block sums by the last wave to arrive (no barrier)
+  // two-level block prefix: every block (workgroup of 4 chunks) also adds its
+  // sum to super_sums[block >> sb_shift]; k_cloud's offset = the super-block
+  // sums before its super-block + the block sums before it inside it
+  unsigned* super_sums;    // zeroed before the launch (by the previous launch's k_decode)
+  unsigned* super_zero;    // the next launch's super-block sums: zeroed by this launch's k_decode
+  int super_cap;           // entries of each super buffer
+  int sb_shift;
 };
 
 // ---------------------------------------------------------------- helpers ----
@@ -461,7 +468,8 @@ __device__ __forceinline__ uint32_t mask4(uint32_t w, uint32_t b, uint32_t tw2, 
 #endif
 constexpr bool kDecYnLds = SLGPU_DEC_YN_LDS != 0;  // yn in LDS (else one early global load per lane)
 constexpr int kDecPl = 2048, kDecX = 4096, kDecY = 4096;
-constexpr int kBsSlots = 16;  // k_decode M_DECIDE: chunk-group iterations per workgroup with a barrier-free block sum
+constexpr int kBsSlots = 64;
+constexpr int kSuperCap = 4096;  // super-block sums per launch group (>= sqrt of its blocks)  // k_decode M_DECIDE: chunk-group iterations per workgroup with a barrier-free block sum
 constexpr int kDecodeLds = (kDecPl * 4 + kDecX + (kDecYnLds ? kDecY : 0)) * 4;  // bytes: > the histogram replicas
 static_assert(kDecodeLds >= 256 * kHistStride * 4, "the decode LDS holds the histogram replicas too");
 
@@ -524,6 +532,9 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   uint32_t tc2 = static_cast<uint32_t>(10 + 17) * 0x00010001u;     // multi_point_cloud_process.py:36-38
   int it = 0;
 
+  // the next launch's super-block sums (scratch of this one)
+  if (p.super_zero && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = tid; i < p.super_cap; i += kThreads) p.super_zero[i] = 0u;
   // the next launch's histogram (scratch of this one)
   if (hist && blockIdx.x == 0)
     for (int i = tid; i < kSlot; i += kThreads) p.hist_zero[view * kSlot + i] = 0u;
@@ -770,8 +781,12 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
             // the workgroup's block sum without a barrier: the last of its
             // waves to add its count (one LDS slot per iteration) writes it
             const unsigned old = atomicAdd(&s_bsum[it], (1u << 16) | mine);
-            if ((old >> 16) == kWaves - 1)
-              p.block_sums[static_cast<int64_t>(view) * ngroups + cg] = static_cast<int>((old & 0xffffu) + mine);
+            if ((old >> 16) == kWaves - 1) {
+              const int64_t blk = static_cast<int64_t>(view) * ngroups + cg;
+              const unsigned t = (old & 0xffffu) + mine;
+              p.block_sums[blk] = static_cast<int>(t);
+              if (t) atomicAdd(p.super_sums + (blk >> p.sb_shift), t);
+            }
           } else {
             s_cnt[it & 1][wid] = static_cast<int>(mine);
           }
@@ -818,7 +833,9 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
       int t = 0;
 #pragma unroll
       for (int w = 0; w < kWaves; ++w) t += s_cnt[it & 1][w];
-      p.block_sums[static_cast<int64_t>(view) * ngroups + cg] = t;
+      const int64_t blk = static_cast<int64_t>(view) * ngroups + cg;
+      p.block_sums[blk] = t;
+      if (t) atomicAdd(p.super_sums + (blk >> p.sb_shift), static_cast<unsigned>(t));
     }
   }
   ++it;
@@ -1122,7 +1139,9 @@ __global__ __launch_bounds__(kThreads, SLGPU_COUNT_WAVES) void k_count(Params p)
     int t = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) t += s_sum[w];
-    p.block_sums[static_cast<int64_t>(view) * gridDim.x + blockIdx.x] = t;
+    const int64_t blk = static_cast<int64_t>(view) * gridDim.x + blockIdx.x;
+    p.block_sums[blk] = t;
+    if (t) atomicAdd(p.super_sums + (blk >> p.sb_shift), static_cast<unsigned>(t));
   }
 }
 
@@ -1545,9 +1564,19 @@ __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
   const int view = blockIdx.y;
   const int civ = blockIdx.x * kWaves + wid;
   const int64_t b = static_cast<int64_t>(view) * gridDim.x + blockIdx.x;  // block index in the launch
-  // ---- block offset: all loads of a batch in flight together ----
+  // ---- block offset: the super-block sums before this block's super-block,
+  // then the block sums before it inside it (both <= ~sqrt(blocks) entries;
+  // all loads of a batch in flight together) ----
   long long acc = 0;
-  for (int64_t t0 = 0; t0 < b; t0 += kPrefixBatch * kThreads) {
+  const int64_t sb = b >> p.sb_shift;
+  for (int64_t t0 = 0; t0 < sb; t0 += kPrefixBatch * kThreads) {
+    unsigned v[kPrefixBatch];
+#pragma unroll
+    for (int i = 0; i < kPrefixBatch; ++i) v[i] = p.super_sums[min<int64_t>(t0 + i * kThreads + tid, sb - 1)];
+#pragma unroll
+    for (int i = 0; i < kPrefixBatch; ++i) acc += (t0 + i * kThreads + tid < sb) ? v[i] : 0u;
+  }
+  for (int64_t t0 = sb << p.sb_shift; t0 < b; t0 += kPrefixBatch * kThreads) {
     int v[kPrefixBatch];
 #pragma unroll
     for (int i = 0; i < kPrefixBatch; ++i) v[i] = p.block_sums[min<int64_t>(t0 + i * kThreads + tid, b - 1)];
@@ -1598,6 +1627,8 @@ struct sl_ctx {
   int64_t cap_cc = 0;
   int* d_block_sums = nullptr;
   int64_t cap_bs = 0;
+  unsigned* d_super[2] = {nullptr, nullptr};  // super-block sums, parity double-buffered (kSuperCap each)
+  int spar = 0;
   uint8_t* d_ptnib = nullptr;
   int64_t cap_ptnib = 0;
   uint16_t* d_codes = nullptr;  // k_decode -> k_count / k_cloud records
@@ -1732,6 +1763,11 @@ int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes) {
   r = grow(c, &c->d_ptnib, &c->cap_ptnib, chunks * kChunkNib);
   if (r) return r;
   for (int b = 0; b < 2; ++b) {
+    int64_t cap = c->d_super[b] ? kSuperCap : 0;
+    r = grow(c, &c->d_super[b], &cap, kSuperCap);  // zeroed once; then by the kernels
+    if (r) return r;
+  }
+  for (int b = 0; b < 2; ++b) {
     const int64_t before = c->cap_hist[b];
     r = grow(c, &c->d_hist[b], &c->cap_hist[b], views * kHistView);  // k_stats' replicas (k_decode's: kSlot)
     if (r) return r;
@@ -1835,6 +1871,16 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->par = b;
     }
     const dim3 grid(static_cast<unsigned>((cpv + kWaves - 1) / kWaves), static_cast<unsigned>(nv));
+    {  // super-block size: the smallest power of two >= sqrt(blocks of the group)
+      const int64_t nb = static_cast<int64_t>(grid.x) * nv;
+      int sh = 0;
+      while ((int64_t{1} << (2 * sh)) < nb) ++sh;
+      p.sb_shift = sh;
+      p.super_sums = c->d_super[c->spar];
+      p.super_zero = c->d_super[c->spar ^ 1];
+      p.super_cap = kSuperCap;
+      c->spar ^= 1;
+    }
     c->last.valid = true;
     dim3 dgrid = grid;  // k_decode: chunk groups strided over a capped grid
     if (c->decode_wgs > 0) dgrid.x = std::min(grid.x, static_cast<unsigned>(std::max(1, (c->decode_wgs + nv - 1) / nv)));
@@ -2072,7 +2118,8 @@ void sl_ctx_destroy(sl_ctx* c) {
                     static_cast<void*>(c->d_nc), static_cast<void*>(c->d_stats), static_cast<void*>(c->d_f32),
                     static_cast<void*>(c->d_codes), static_cast<void*>(c->d_hist[0]),
                     static_cast<void*>(c->d_hist[1]), static_cast<void*>(c->d_ptnib),
-                    static_cast<void*>(c->d_block_sums), static_cast<void*>(c->d_chunk_counts)})
+                    static_cast<void*>(c->d_block_sums), static_cast<void*>(c->d_chunk_counts),
+                    static_cast<void*>(c->d_super[0]), static_cast<void*>(c->d_super[1])})
     if (ptr) (void)hipFree(ptr);
   delete c;
 }
@@ -2379,12 +2426,15 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
   hipEvent_t ev[4];
   for (int k = 0; k < 4; ++k) HIP_TRY(c, hipEventCreate(&ev[k]));
   int r = SL_OK;
-  // k_count and k_cloud first: they read k_decode's records and histogram,
-  // which k_decode's re-runs then overwrite (records identically; the
-  // histograms accumulate and are reset below)
+  // k_cloud, then k_count, then k_decode: the consumers first -- k_cloud reads
+  // the block and super-block sums (which the producers' re-runs add into
+  // again) and k_decode's records; k_count reads the histogram k_decode's
+  // re-runs accumulate into (reset below)
   // (M_DECIDE: k_cloud, then k_decode -- it reads the histograms k_stats'
   // re-runs accumulate into -- then k_stats)
-  const int order3[3] = {1, 2, 0}, orderd[3] = {2, 0, 1};
+  // k_cloud re-runs first in both paths: the producers' re-runs (k_count /
+  // k_decode) add their block sums into the super-block sums again
+  const int order3[3] = {2, 1, 0}, orderd[3] = {2, 0, 1};
   const int* order = c->last.decide ? orderd : order3;
   HIP_TRY(c, hipEventRecord(ev[0], s));
   for (int q = 0; q < 3 && r == SL_OK; ++q) {
