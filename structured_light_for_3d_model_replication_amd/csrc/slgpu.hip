@@ -509,6 +509,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   __shared__ int s_max[kWaves];
   __shared__ int s_cnt[2][kWaves];
   __shared__ unsigned s_bsum[kBsSlots];  // per iteration: points (low 16 bits) + waves arrived << 16
+  __shared__ uint32_t s_thr[2];          // M_DECIDE adaptive: the view's tw2, tc2
   unsigned* s_hist = s_lds;
   float4* s_pl = reinterpret_cast<float4*>(s_lds);
   float* s_xn = reinterpret_cast<float*>(s_lds) + 4 * kDecPl;
@@ -521,15 +522,34 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   const int64_t HW = p.HW;
   if (decide) {
     if (tid < kBsSlots) s_bsum[tid] = 0u;
+    // the view's mask thresholds (k_stats' histograms), once per workgroup by
+    // wave 0 while the others fill the tables: at this point no decode state
+    // is live (computed inside the chunk loop they cost registers and ~9 us)
+    if ((mode & M_HIST) && wid == 0) {
+      const Thresholds t = view_thresholds(p, view, lane);
+      if (lane == 0) {
+        s_thr[0] = static_cast<uint32_t>(t.white + 1) * 0x00010001u;
+        s_thr[1] = static_cast<uint32_t>(t.contrast + 17) * 0x00010001u;
+        if (blockIdx.x == 0) {
+          p.stats[view].thr_white = t.white;
+          p.stats[view].thr_contrast = t.contrast;
+          p.stats[view].noise_floor = t.noise_floor;
+          p.stats[view].dynamic_range = t.dynamic_range;
+        }
+      }
+    }
     for (int i = tid; i < p.Wp; i += kThreads) s_pl[i] = p.planes32[i];
     for (int i = tid; i < p.W; i += kThreads) s_xn[i] = p.xn32[i];
     if (kDecYnLds)
       for (int i = tid; i < p.H; i += kThreads) s_yn[i] = p.yn32[i];
     __syncthreads();
   }
-  int cur_view = -1;                                               // M_DECIDE: the wave's thresholds
   uint32_t tw2 = static_cast<uint32_t>(40 + 1) * 0x00010001u;      // fixed mask:
   uint32_t tc2 = static_cast<uint32_t>(10 + 17) * 0x00010001u;     // multi_point_cloud_process.py:36-38
+  if (decide && (mode & M_HIST)) {  // adaptive: the view's (wave 0 above; the table fill's barrier)
+    tw2 = __builtin_amdgcn_readfirstlane(s_thr[0]);
+    tc2 = __builtin_amdgcn_readfirstlane(s_thr[1]);
+  }
   int it = 0;
 
   // the next launch's super-block sums (scratch of this one)
@@ -698,19 +718,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
       }
     }
     if (decide) {
-      // ---- mask with the view's thresholds (wave-cached; k_stats' histograms) ----
-      if ((mode & M_HIST) && view != cur_view) {
-        const Thresholds t = view_thresholds(p, view, lane);
-        tw2 = static_cast<uint32_t>(t.white + 1) * 0x00010001u;
-        tc2 = static_cast<uint32_t>(t.contrast + 17) * 0x00010001u;
-        if (civ == 0 && lane == 0) {
-          p.stats[view].thr_white = t.white;
-          p.stats[view].thr_contrast = t.contrast;
-          p.stats[view].noise_floor = t.noise_floor;
-          p.stats[view].dynamic_range = t.dynamic_range;
-        }
-        cur_view = view;
-      }
+      // ---- mask with the view's thresholds (tw2 / tc2: computed at kernel start) ----
       uint32_t ok = 0u, mb[4];
 #pragma unroll
       for (int w = 0; w < 4; ++w) ok |= mask4(word(wq, w), word(bq, w), tw2, tc2, &mb[w]) << (4 * w);
