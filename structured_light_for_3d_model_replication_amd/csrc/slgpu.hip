@@ -116,6 +116,7 @@ constexpr int M_NC = 16;       // rays from a device Nc table instead of pinhole
 constexpr int M_ROWS = 32;     // k_decode: decode the row sequence
 constexpr int M_HIST = 64;     // adaptive mask: k_decode builds the histogram, k_count reads it
 constexpr int M_FAST32 = 128;  // k_cloud: f32 arithmetic for well-conditioned points (SL_XYZ_F32_FAST)
+constexpr int M_PLANE_RSRC = 512;  // k_decode: a buffer descriptor per plane (a view's planes read span >= 2 GiB)
 constexpr int M_DECIDE = 256;  // k_decode: also the mask and the |n.r| decision (k_count's work; k_stats
                                // histograms): mask map, point nibbles, chunk counts, block sums
 constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
@@ -151,7 +152,7 @@ static_assert(sizeof(ViewStats) % 64 == 0, "ViewStats keeps 64-B alignment");
 struct Params {
   const uint8_t* stack;
   int64_t stack_vs;
-  int view_bytes;  // min(n_img * H * W, 2^31 - 1) (informational; k_decode uses a descriptor per plane)
+  int view_bytes;  // bytes of a view's planes k_decode reads (< 2^31 unless M_PLANE_RSRC)
   const uint8_t* tex;
   int64_t tex_vs;
   const int32_t* in_col;
@@ -601,11 +602,19 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   } else {
     // Plane loads: on the vector path a buffer descriptor of the view's stack
     // (SGPRs) + the lane's 32-bit pixel offset + the plane offset in an SGPR.
+    // When the planes read span 2 GiB or more (M_PLANE_RSRC), a descriptor per
+    // plane instead (4 SGPRs each: 46 planes overflow the SGPR file, so this is
+    // not the default).
     const uint8_t* vbase = p.stack + view * p.stack_vs;
     const int voff = static_cast<int>(pxl);
+    const __amdgpu_buffer_rsrc_t rs_view =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vbase), 0, p.view_bytes, 0x00020000);
     auto ldp = [&](int plane) -> uint4 {
+      if (vec && !(mode & M_PLANE_RSRC)) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_view, voff, plane * static_cast<int>(HW), kLoadAux);
+        return make_uint4(v[0], v[1], v[2], v[3]);
+      }
       if (vec) {
-        // a descriptor per plane (SGPRs): one plane, not the view's stack, must be < 2 GiB
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint8_t*>(vbase) + static_cast<int64_t>(plane) * HW, 0, static_cast<int>(HW), 0x00020000);
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, kLoadAux);
@@ -2312,7 +2321,9 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   fill_common(c, p, n_views, H, W);
   p.stack = stack;
   p.stack_vs = stack_vs;
-  p.view_bytes = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(n_img) * HW, INT32_MAX));
+  const int64_t read_bytes = static_cast<int64_t>(2 + 2 * pairs) * HW;  // the planes k_decode reads
+  const int plane_rsrc = read_bytes >= (1ll << 31) ? M_PLANE_RSRC : 0;
+  p.view_bytes = static_cast<int>(std::min<int64_t>(read_bytes, INT32_MAX));
   p.tex = tex;
   p.tex_vs = tex_vs;
   p.nc = nc;
@@ -2328,7 +2339,7 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   p.view_offsets = view_offsets;
   const int nc_bit = (xyz && c->d_nc) ? M_NC : 0;
   const int hist_bit = mask_mode == SL_MASK_ADAPTIVE ? M_HIST : 0;
-  const int decode_mode = (maps ? (M_MAPS | M_ROWS) : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit;
+  const int decode_mode = (maps ? (M_MAPS | M_ROWS) : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit | plane_rsrc;
   const int count_mode = (maps ? M_MAPS : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit;
   const int cloud_mode = xyz ? xyz_mode_bits(c, xyz_dtype, poses) : -1;
   const bool vec = (W % 16 == 0) && W >= 64 && aligned16(stack) && (stack_vs % 16 == 0) &&
