@@ -176,6 +176,8 @@ struct Params {
   double o0, o1, o2;       // Oc
   const double* poses;
   uint16_t* codes;   // [view][HW] records: min(col, Wp-1)
+  const int32_t* rec_col;  // maps + cloud on the decide path: k_cloud takes min(col, Wp-1) from this col
+                           // map and k_decode writes no records (2 B/px less k_decode write traffic)
   uint8_t* ptnib;    // [chunk][4 steps][64 lanes] point nibbles: bit e of byte (s, l) = pixel 256 s + 4 l + e
   int32_t* col_out;
   int32_t* row_out;
@@ -825,7 +827,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
     }
   }
 
-  if (mode & M_CODES) {
+  if ((mode & M_CODES) && !p.rec_col) {
     // records for k_count / k_cloud: clipped column code
     uint32_t rec[kPx / 2];
 #pragma unroll
@@ -1231,23 +1233,45 @@ __device__ __forceinline__ void chunk_uv(int u_c, int v_c, int local, int W, int
   *v = vv;
 }
 
-// One chunk (global index gc, output offset base) of k_cloud, by one wave.
-template <int MODE, int VEC>
-__device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane,
-                                            uint32_t* s_ent, uint32_t* s_bgr, float* s_sxyz, uint8_t* s_scol) {
+// A lane's inputs of one k_cloud chunk: records, colour bytes, point bits.
+struct ChunkIn {
+  uint32_t d[kPx / 2];  // records (clipped column codes), 2 per word
+  uint4 tq[3];          // BGR bytes of the 16 pixels (or the white plane's in tq[0])
+  uint32_t nb4;         // point nibbles of the 16 pixels
+};
+
+// Phase 1 of a chunk (global index gc): the lane's loads, issued by k_cloud
+// before its block-offset loads so that both round trips overlap.
+template <int VEC>
+__device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane, ChunkIn* in) {
   const bool vec = VEC > 0;
   const int view = static_cast<int>(gc / p.cpv);
   const int civ = static_cast<int>(gc - static_cast<int64_t>(view) * p.cpv);
   const int64_t HW = p.HW;
-  const int64_t cpx = static_cast<int64_t>(civ) * kChunk;  // chunk's first pixel
-  const int64_t px0 = cpx + lane * kPx;
+  const int64_t px0 = static_cast<int64_t>(civ) * kChunk + lane * kPx;
   const int n_px = static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx));
   const int64_t pxl = n_px > 0 ? px0 : 0;
-  __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads come first
-
-  // ---- 1. records + colour, streaming layout ----
-  uint32_t d[kPx / 2];
-  {
+  uint32_t* d = in->d;
+  if (p.rec_col) {  // the col map k_decode wrote, clipped (sl_system.py:626)
+    const int32_t* src = p.rec_col + view * HW + pxl;
+    const uint32_t cmax = static_cast<uint32_t>(p.Wp - 1);
+    uint32_t c[kPx];
+    if (vec) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint4 q = ld_side16(src + 4 * i);
+        c[4 * i] = q.x;
+        c[4 * i + 1] = q.y;
+        c[4 * i + 2] = q.z;
+        c[4 * i + 3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) c[k] = k < n_px ? static_cast<uint32_t>(src[k]) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < kPx / 2; ++i) d[i] = min(c[2 * i], cmax) | (min(c[2 * i + 1], cmax) << 16);
+  } else {
     const uint16_t* src = p.codes + view * HW + pxl;
     if (vec) {
       const uint4 a = ld_side16(src);
@@ -1265,9 +1289,8 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   }
   // colour: BGR texture, or the white plane replicated (the colour imread of a
   // single-channel file 0, sl_system.py:580)
-  uint4 tq[3];
-  const bool has_tex = p.tex != nullptr;
-  if (has_tex) {
+  uint4* tq = in->tq;
+  if (p.tex != nullptr) {
     const uint8_t* t = p.tex + view * p.tex_vs + 3 * pxl;
     if (vec) {
       tq[0] = ld_side16(t);
@@ -1284,7 +1307,22 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   }
   // the lane's 16 point bits (k_count): the nibbles of pixels 16 l .. 16 l + 15,
   // bytes 64 (l / 16) + 4 (l % 16) + 0..3 of the chunk
-  const uint32_t nb4 = *reinterpret_cast<const uint32_t*>(p.ptnib + gc * kChunkNib + 64 * (lane >> 4) + 4 * (lane & 15));
+  in->nb4 = *reinterpret_cast<const uint32_t*>(p.ptnib + gc * kChunkNib + 64 * (lane >> 4) + 4 * (lane & 15));
+}
+
+// Phases 2-3 of a chunk (global index gc, output offset base), by one wave,
+// from the lane's loads.
+template <int MODE>
+__device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane, const ChunkIn& in,
+                                            uint32_t* s_ent, uint32_t* s_bgr, float* s_sxyz, uint8_t* s_scol) {
+  const int view = static_cast<int>(gc / p.cpv);
+  const int civ = static_cast<int>(gc - static_cast<int64_t>(view) * p.cpv);
+  const int64_t cpx = static_cast<int64_t>(civ) * kChunk;  // chunk's first pixel
+  const bool has_tex = p.tex != nullptr;
+  const uint32_t* d = in.d;
+  const uint4* tq = in.tq;
+  const uint32_t nb4 = in.nb4;
+  __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads come first
   const uint32_t ptbits = (nb4 & 0xfu) | ((nb4 >> 4) & 0xf0u) | ((nb4 >> 8) & 0xf00u) | ((nb4 >> 12) & 0xf000u);
   const int n_l = __popc(ptbits);
   const int incl = wave_incl_scan(n_l, lane);
@@ -1567,6 +1605,10 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
 // groups of the call); each wave adds the counts of the chunks before it in
 // the workgroup.
 constexpr int kPrefixBatch = 4;
+#ifndef SLGPU_CLOUD_HOIST
+#define SLGPU_CLOUD_HOIST 0
+#endif
+constexpr bool kCloudHoist = SLGPU_CLOUD_HOIST != 0;  // chunk loads issued before the block-offset loads
 
 template <int MODE, int VEC>
 __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
@@ -1581,6 +1623,11 @@ __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
   const int view = blockIdx.y;
   const int civ = blockIdx.x * kWaves + wid;
   const int64_t b = static_cast<int64_t>(view) * gridDim.x + blockIdx.x;  // block index in the launch
+  const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
+  // the chunk's own loads first: they do not depend on its offset, so their
+  // round trip overlaps the one of the offset's loads below
+  ChunkIn in;
+  if (kCloudHoist && civ < p.cpv) cloud_load<VEC>(p, gc, lane, &in);
   // ---- block offset: the super-block sums before this block's super-block,
   // then the block sums before it inside it (both <= ~sqrt(blocks) entries;
   // all loads of a batch in flight together) ----
@@ -1600,7 +1647,6 @@ __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
 #pragma unroll
     for (int i = 0; i < kPrefixBatch; ++i) acc += (t0 + i * kThreads + tid < b) ? v[i] : 0;
   }
-  const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
   const int before = (lane < wid && civ < p.cpv) ? p.chunk_counts[gc - wid + lane] : 0;  // earlier waves' chunks
   acc = wave_sum64(acc);
   if (lane == 0) s_wred[wid] = acc;
@@ -1611,9 +1657,10 @@ __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
   base += wave_sum(before);
   base = uniform64(base);
   if (civ >= p.cpv) return;
+  if (!kCloudHoist) cloud_load<VEC>(p, gc, lane, &in);
   if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1)
     p.view_offsets[p.n_views] = base + p.chunk_counts[gc];
-  cloud_chunk<MODE, VEC>(p, gc, base, lane, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0]);
+  cloud_chunk<MODE>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0]);
 }
 
 }  // namespace
@@ -1658,6 +1705,7 @@ struct sl_ctx {
   std::vector<char> prof_decide;    // per call: M_DECIDE path (events around k_stats, k_decode, k_cloud)
   int n_cu = 0;
   bool force_3k = false;            // SLGPU_PATH=3: k_decode + k_count + k_cloud for aligned frames too (A/B)
+  bool rec_from_maps = true;        // maps + cloud: k_cloud reads the col map (SLGPU_RECORDS=1: records, A/B)
   int prof_n = 0;
   // the last launch group's kernels and arguments (sl_time_kernels)
   // RCCL gather (sl_gather_init): communicator, this rank, count scratch
@@ -1873,6 +1921,8 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     p.base_in = (v0 > 0 && p.view_offsets) ? p.view_offsets : nullptr;
     p.stats = c->d_stats + v0;
     p.codes = c->d_codes;
+    // maps + cloud on the decide path: k_cloud reads the col map (no records)
+    p.rec_col = (decide && p.col_out && cloud_mode >= 0 && c->rec_from_maps) ? p.col_out : nullptr;
     p.ptnib = c->d_ptnib;
     p.chunk_counts = c->d_chunk_counts;
     p.block_sums = c->d_block_sums;
@@ -2114,6 +2164,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
   c->n_cu = n_cu;
   if (per_cu > 0) c->decode_wgs = per_cu * n_cu;
   if (const char* d = getenv("SLGPU_PATH")) c->force_3k = atoi(d) == 3;
+  if (const char* d = getenv("SLGPU_RECORDS")) c->rec_from_maps = atoi(d) != 1;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
