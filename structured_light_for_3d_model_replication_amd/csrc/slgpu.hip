@@ -117,6 +117,7 @@ constexpr int M_ROWS = 32;     // k_decode: decode the row sequence
 constexpr int M_HIST = 64;     // adaptive mask: k_decode builds the histogram, k_count reads it
 constexpr int M_FAST32 = 128;  // k_cloud: f32 arithmetic for well-conditioned points (SL_XYZ_F32_FAST)
 constexpr int M_PLANE_RSRC = 512;  // k_decode: a buffer descriptor per plane (a view's planes read span >= 2 GiB)
+constexpr int M_TEX = 2048;    // k_cloud: a BGR texture (else the white plane replicated)
 constexpr int M_DECIDE = 256;  // k_decode: also the mask and the |n.r| decision (k_count's work; k_stats
                                // histograms): mask map, point nibbles, chunk counts, block sums
 constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
@@ -470,6 +471,10 @@ __device__ __forceinline__ uint32_t mask4(uint32_t w, uint32_t b, uint32_t tw2, 
 #define SLGPU_DEC_YN_LDS 0
 #endif
 constexpr bool kDecYnLds = SLGPU_DEC_YN_LDS != 0;  // yn in LDS (else one early global load per lane)
+#ifndef SLGPU_DEC_GLDS
+#define SLGPU_DEC_GLDS 0
+#endif
+constexpr bool kDecGlds = SLGPU_DEC_GLDS != 0;  // decision tables by LDS-DMA, overlapping the first stack loads
 constexpr int kDecPl = 2048, kDecX = 4096, kDecY = 4096;
 constexpr int kBsSlots = 64;
 constexpr int kSuperCap = 4096;  // super-block sums per launch group (>= sqrt of its blocks)  // k_decode M_DECIDE: chunk-group iterations per workgroup with a barrier-free block sum
@@ -541,15 +546,28 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         }
       }
     }
-    for (int i = tid; i < p.Wp; i += kThreads) s_pl[i] = p.planes32[i];
-    for (int i = tid; i < p.W; i += kThreads) s_xn[i] = p.xn32[i];
+    if (kDecGlds) {
+      // the tables by LDS-DMA (16 B per lane, 1 KB per wave instruction): no
+      // VGPRs, and the first chunk group's stack loads below are issued
+      // while they land; the workgroup barrier before the first mask
+      // (iteration 0) publishes them.  Lanes past the end repeat the last
+      // entry into slack LDS (kDecPl, kDecX are multiples of 64 entries).
+      typedef __attribute__((address_space(3))) void* lds_ptr_t;
+      for (int i = wid; i * 64 < p.Wp; i += kWaves)
+        __builtin_amdgcn_global_load_lds(p.planes32 + min(i * 64 + lane, p.Wp - 1), (lds_ptr_t)(s_pl + i * 64), 16, 0, 0);
+      for (int i = wid; i * 256 < p.W; i += kWaves)
+        __builtin_amdgcn_global_load_lds(p.xn32 + min(i * 256 + 4 * lane, p.W - 4), (lds_ptr_t)(s_xn + i * 256), 16, 0, 0);
+    } else {
+      for (int i = tid; i < p.Wp; i += kThreads) s_pl[i] = p.planes32[i];
+      for (int i = tid; i < p.W; i += kThreads) s_xn[i] = p.xn32[i];
+    }
     if (kDecYnLds)
       for (int i = tid; i < p.H; i += kThreads) s_yn[i] = p.yn32[i];
-    __syncthreads();
+    if (!kDecGlds) __syncthreads();
   }
   uint32_t tw2 = static_cast<uint32_t>(40 + 1) * 0x00010001u;      // fixed mask:
   uint32_t tc2 = static_cast<uint32_t>(10 + 17) * 0x00010001u;     // multi_point_cloud_process.py:36-38
-  if (decide && (mode & M_HIST)) {  // adaptive: the view's (wave 0 above; the table fill's barrier)
+  if (!kDecGlds && decide && (mode & M_HIST)) {  // adaptive: the view's (wave 0 above; the table fill's barrier)
     tw2 = __builtin_amdgcn_readfirstlane(s_thr[0]);
     tc2 = __builtin_amdgcn_readfirstlane(s_thr[1]);
   }
@@ -729,6 +747,13 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
       }
     }
     if (decide) {
+      if (kDecGlds && it == 0) {  // workgroup-uniform: the LDS-DMA tables and s_thr are in
+        __syncthreads();
+        if (mode & M_HIST) {
+          tw2 = __builtin_amdgcn_readfirstlane(s_thr[0]);
+          tc2 = __builtin_amdgcn_readfirstlane(s_thr[1]);
+        }
+      }
       // ---- mask with the view's thresholds (tw2 / tc2: computed at kernel start) ----
       uint32_t ok = 0u, mb[4];
 #pragma unroll
@@ -1212,12 +1237,20 @@ __device__ __forceinline__ T* at_bytes(T* base, unsigned off) {
   return reinterpret_cast<T*>(reinterpret_cast<B*>(base) + off);
 }
 
-// Pixel (u, v) of chunk-local pixel `local` (the chunk starts at (u_c, v_c)):
-// one row wrap at most when W >= kChunk (wave-uniform test), else a loop.
+// Pixel (u, v) of the entry's chunk-local pixel (the chunk starts at (u_c,
+// v_c)): the 16-byte path carries the row offset in the entry; otherwise one
+// row wrap at most when W >= kChunk (wave-uniform test), else a loop.
+__device__ __forceinline__ uint32_t ent_code(uint32_t e) { return (e >> 10) & 0x7fffu; }
 // The range facts let the table gathers use 32-bit offsets.
-__device__ __forceinline__ void chunk_uv(int u_c, int v_c, int local, int W, int* u, int* v) {
+template <int VEC>
+__device__ __forceinline__ void chunk_uv(int u_c, int v_c, uint32_t e, int W, int* u, int* v) {
+  const int local = static_cast<int>(e & 1023u);
   int uu = u_c + local, vv = v_c;
-  if (W >= kChunk) {
+  if (VEC > 0) {  // the entry's row offset (cloud_chunk)
+    const int dr = static_cast<int>(e >> 25);
+    uu -= dr * W;
+    vv += dr;
+  } else if (W >= kChunk) {
     const bool wrap = uu >= W;
     uu -= wrap ? W : 0;
     vv += wrap ? 1 : 0;
@@ -1312,13 +1345,22 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
 
 // Phases 2-3 of a chunk (global index gc, output offset base), by one wave,
 // from the lane's loads.
-template <int MODE>
+template <int MODE, int VEC>
 __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane, const ChunkIn& in,
                                             uint32_t* s_ent, uint32_t* s_bgr, float* s_sxyz, uint8_t* s_scol) {
   const int view = static_cast<int>(gc / p.cpv);
   const int civ = static_cast<int>(gc - static_cast<int64_t>(view) * p.cpv);
   const int64_t cpx = static_cast<int64_t>(civ) * kChunk;  // chunk's first pixel
-  const bool has_tex = p.tex != nullptr;
+  const int mode = MODE >= 0 ? MODE : p.mode;
+  const bool has_tex = (mode & M_TEX) != 0;
+  // 16-byte path (W % 16 == 0, W >= 64): a lane's 16 pixels share one image
+  // row, at most 17 rows below the chunk's first; the row offset rides in
+  // the entry (bits 25..29) so that cloud_points needs no division
+  uint32_t drow = 0u;
+  if (VEC > 0) {
+    const int px = static_cast<int>(cpx) + lane * kPx;  // < HW < 2^31
+    drow = static_cast<uint32_t>(px / p.W - static_cast<int>(cpx) / p.W) << 25;
+  }
   const uint32_t* d = in.d;
   const uint4* tq = in.tq;
   const uint32_t nb4 = in.nb4;
@@ -1358,7 +1400,7 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
         bgr = byte_of(tq[0], k) * 0x010101u;
       }
       if ((ptbits >> k) & 1u) {
-        s_ent[idx] = static_cast<uint32_t>(lane * kPx + k) | (code << 10);
+        s_ent[idx] = static_cast<uint32_t>(lane * kPx + k) | (code << 10) | drow;
         if (kLdsBgr) s_bgr[idx] = bgr;
         (void)bgr;
       }
@@ -1368,18 +1410,19 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   __builtin_amdgcn_wave_barrier();
   if (kAblate & 16) return;  // measurement only: stop after the LDS compaction
 
-  cloud_points<MODE>(p, view, cpx, base, lane, total, s_ent, s_bgr, s_sxyz, s_scol);
+  cloud_points<MODE, VEC>(p, view, cpx, base, lane, total, s_ent, s_bgr, s_sxyz, s_scol);
 }
 
-// Phase 3 of a chunk: its `total` compacted points (s_ent: pixel | code << 10,
-// s_bgr: colour) -> xyz + BGR at offset base + rank, kPipe x 64 per pass.
-template <int MODE>
+// Phase 3 of a chunk: its `total` compacted points (s_ent: pixel | code << 10
+// | row offset << 25 on the 16-byte path, s_bgr: colour) -> xyz + BGR at
+// offset base + rank, kPipe x 64 per pass.
+template <int MODE, int VEC>
 __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
                                              int total, const uint32_t* s_ent, const uint32_t* s_bgr,
                                              float* s_sxyz, uint8_t* s_scol) {
   const int mode = MODE >= 0 ? MODE : p.mode;
   const int64_t HW = p.HW;
-  const bool has_tex = p.tex != nullptr;
+  const bool has_tex = (mode & M_TEX) != 0;
   // r = (x, y, 1) / sqrt((x*x + y*y) + 1) (sl_system.py:614-621) or Nc
   // (:605-606), plane of the clipped code (:624-633), den = (n0 r0 + n1 r1) +
   // n2 r2 (:638), t = -(n.Oc + d) / den (:639, :643; n.Oc + d per plane,
@@ -1426,16 +1469,16 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         const int local = static_cast<int>(e & 1023u);
         bgr[i] = point_bgr(j, local);
         int uu, vv;
-        chunk_uv(u_c, v_c, local, W, &uu, &vv);
+        chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
         if (kAblate & 512) {  // measurement only: no table gathers
           fx[i] = 0.001f * static_cast<float>(uu);
           fy[i] = 0.001f * static_cast<float>(vv);
-          fp[i] = make_float4(0.1f, 0.2f, 0.9f, -500.0f - static_cast<float>(e >> 10));
+          fp[i] = make_float4(0.1f, 0.2f, 0.9f, -500.0f - static_cast<float>(ent_code(e)));
           continue;
         }
         fx[i] = *at_bytes(p.xn32, 4u * static_cast<unsigned>(uu));
         fy[i] = *at_bytes(p.yn32, 4u * static_cast<unsigned>(vv));
-        fp[i] = p.planes32[e >> 10];
+        fp[i] = p.planes32[ent_code(e)];
       }
 #pragma unroll
       for (int i = 0; i < kPipe; ++i) {
@@ -1455,9 +1498,9 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         } else {  // ill-conditioned: exact f64, as the path below
           const uint32_t e = s_ent[min(j, total - 1)];
           int uu, vv;
-          chunk_uv(u_c, v_c, static_cast<int>(e & 1023u), W, &uu, &vv);
+          chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
           const double xd = p.xn[uu], yd = p.yn[vv];
-          const double4 pd = p.planes[e >> 10];
+          const double4 pd = p.planes[ent_code(e)];
           const double nrm = sqrt((xd * xd + yd * yd) + 1.0);
           const double d0 = xd / nrm, d1 = yd / nrm, d2 = 1.0 / nrm;
           const double td = -pd.w / ((pd.x * d0 + pd.y * d1) + pd.z * d2);
@@ -1489,7 +1532,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       const uint32_t e = s_ent[j];
       const int local = static_cast<int>(e & 1023u);
       bgr[i] = point_bgr(j, local);
-      const unsigned c = e >> 10;
+      const unsigned c = ent_code(e);
       if (dbg & 4) {
         ra[i] = 0.25 + local;
         rb[i] = 0.5;
@@ -1504,7 +1547,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         rcz[i] = p.nc_rays[2 * HW + q];
       } else {
         int uu, vv;
-        chunk_uv(u_c, v_c, local, W, &uu, &vv);
+        chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
         ra[i] = p.xn[uu];
         rb[i] = p.yn[vv];
       }
@@ -1610,27 +1653,12 @@ constexpr int kPrefixBatch = 4;
 #endif
 constexpr bool kCloudHoist = SLGPU_CLOUD_HOIST != 0;  // chunk loads issued before the block-offset loads
 
-template <int MODE, int VEC>
-__global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
-  __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
-  __shared__ __attribute__((aligned(16))) uint32_t s_bgr[kWaves][kBgrWords];  // colours (kBgrMode)
-  __shared__ float s_sxyz[kWaves][kStageOut ? 192 : 1];      // output stage: 64 points' xyz
-  __shared__ uint8_t s_scol[kWaves][kStageOut ? 192 : 4];    // and their colour bytes
-  __shared__ long long s_wred[kWaves];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
-  const int view = blockIdx.y;
-  const int civ = blockIdx.x * kWaves + wid;
-  const int64_t b = static_cast<int64_t>(view) * gridDim.x + blockIdx.x;  // block index in the launch
-  const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
-  // the chunk's own loads first: they do not depend on its offset, so their
-  // round trip overlaps the one of the offset's loads below
-  ChunkIn in;
-  if (kCloudHoist && civ < p.cpv) cloud_load<VEC>(p, gc, lane, &in);
-  // ---- block offset: the super-block sums before this block's super-block,
-  // then the block sums before it inside it (both <= ~sqrt(blocks) entries;
-  // all loads of a batch in flight together) ----
+// Points of the blocks before block b of the launch group (one workgroup;
+// holds a workgroup barrier): the super-block sums before b's super-block,
+// then the block sums before b inside it (both <= ~sqrt(blocks) entries; all
+// loads of a batch in flight together).
+__device__ __forceinline__ long long block_offset(const Params& p, int64_t b, int tid, int lane, int wid,
+                                                  long long* s_wred) {
   long long acc = 0;
   const int64_t sb = b >> p.sb_shift;
   for (int64_t t0 = 0; t0 < sb; t0 += kPrefixBatch * kThreads) {
@@ -1647,20 +1675,42 @@ __global__ __launch_bounds__(kThreads) void k_cloud(Params p) {
 #pragma unroll
     for (int i = 0; i < kPrefixBatch; ++i) acc += (t0 + i * kThreads + tid < b) ? v[i] : 0;
   }
-  const int before = (lane < wid && civ < p.cpv) ? p.chunk_counts[gc - wid + lane] : 0;  // earlier waves' chunks
   acc = wave_sum64(acc);
   if (lane == 0) s_wred[wid] = acc;
   __syncthreads();
-  long long base = p.base_in ? *p.base_in : 0ll;
+  long long t = 0;
 #pragma unroll
-  for (int w = 0; w < kWaves; ++w) base += s_wred[w];
+  for (int w = 0; w < kWaves; ++w) t += s_wred[w];
+  return t;
+}
+
+template <int MODE, int VEC>
+__global__ __launch_bounds__(kThreads, 5) void k_cloud(Params p) {
+  __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
+  __shared__ __attribute__((aligned(16))) uint32_t s_bgr[kWaves][kBgrWords];  // colours (kBgrMode)
+  __shared__ float s_sxyz[kWaves][kStageOut ? 192 : 1];      // output stage: 64 points' xyz
+  __shared__ uint8_t s_scol[kWaves][kStageOut ? 192 : 4];    // and their colour bytes
+  __shared__ long long s_wred[kWaves];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
+  const int view = blockIdx.y;
+  const int civ = blockIdx.x * kWaves + wid;
+  const int64_t b = static_cast<int64_t>(view) * gridDim.x + blockIdx.x;  // block index in the launch
+  const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
+  // (SLGPU_CLOUD_HOIST: the chunk's own loads before the offset's; measured slower)
+  ChunkIn in;
+  if (kCloudHoist && civ < p.cpv) cloud_load<VEC>(p, gc, lane, &in);
+  const int before = (lane < wid && civ < p.cpv) ? p.chunk_counts[gc - wid + lane] : 0;  // earlier waves' chunks
+  long long base = block_offset(p, b, tid, lane, wid, s_wred);
+  base += p.base_in ? *p.base_in : 0ll;
   base += wave_sum(before);
   base = uniform64(base);
   if (civ >= p.cpv) return;
   if (!kCloudHoist) cloud_load<VEC>(p, gc, lane, &in);
   if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1)
     p.view_offsets[p.n_views] = base + p.chunk_counts[gc];
-  cloud_chunk<MODE>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0]);
+  cloud_chunk<MODE, VEC>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0]);
 }
 
 }  // namespace
@@ -1873,8 +1923,8 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
 }
 
 KernelFn pick_cloud(int mode, bool vec) {
-  if (vec && mode == 0) return k_cloud<0, 1>;  // f32 xyz, pinhole rays
-  if (vec && mode == M_FAST32) return k_cloud<M_FAST32, 1>;
+  if (vec && mode == M_TEX) return k_cloud<M_TEX, 1>;  // f32 xyz, pinhole rays, BGR texture
+  if (vec && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1>;
   return vec ? k_cloud<-1, 1> : k_cloud<-1, 0>;
 }
 
@@ -2392,7 +2442,7 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   const int hist_bit = mask_mode == SL_MASK_ADAPTIVE ? M_HIST : 0;
   const int decode_mode = (maps ? (M_MAPS | M_ROWS) : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit | plane_rsrc;
   const int count_mode = (maps ? M_MAPS : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit;
-  const int cloud_mode = xyz ? xyz_mode_bits(c, xyz_dtype, poses) : -1;
+  const int cloud_mode = xyz ? (xyz_mode_bits(c, xyz_dtype, poses) | (tex ? M_TEX : 0)) : -1;
   const bool vec = (W % 16 == 0) && W >= 64 && aligned16(stack) && (stack_vs % 16 == 0) &&
                    (!tex || (aligned16(tex) && tex_vs % 16 == 0)) &&
                    (!maps || (aligned16(col_out) && aligned16(row_out) && aligned16(mask_out)));
@@ -2428,7 +2478,7 @@ int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, 
   const int nc_bit = c->d_nc ? M_NC : 0;
   const int decode_mode = M_FROMMAPS | M_CODES | nc_bit;
   const int count_mode = M_FROMMAPS | M_CODES | nc_bit;
-  const int cloud_mode = xyz_mode_bits(c, xyz_dtype, poses);
+  const int cloud_mode = xyz_mode_bits(c, xyz_dtype, poses) | (tex ? M_TEX : 0);
   const bool vec = (W % 16 == 0) && W >= 64 && aligned16(col_map) && aligned16(mask) && aligned16(tex);
   HIP_TRY(c, hipSetDevice(c->device));
   const hipStream_t s = static_cast<hipStream_t>(stream);
