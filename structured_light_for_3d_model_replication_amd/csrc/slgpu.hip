@@ -472,7 +472,7 @@ __device__ __forceinline__ uint32_t mask4(uint32_t w, uint32_t b, uint32_t tw2, 
 #endif
 constexpr bool kDecYnLds = SLGPU_DEC_YN_LDS != 0;  // yn in LDS (else one early global load per lane)
 #ifndef SLGPU_DEC_GLDS
-#define SLGPU_DEC_GLDS 0
+#define SLGPU_DEC_GLDS 1
 #endif
 constexpr bool kDecGlds = SLGPU_DEC_GLDS != 0;  // decision tables by LDS-DMA, overlapping the first stack loads
 constexpr int kDecPl = 2048, kDecX = 4096, kDecY = 4096;
@@ -1209,6 +1209,10 @@ __global__ __launch_bounds__(kThreads, SLGPU_COUNT_WAVES) void k_count(Params p)
 #define SLGPU_PIPE 4
 #endif
 constexpr int kPipe = SLGPU_PIPE;  // points per lane per pass in k_cloud
+#ifndef SLGPU_SMALL_PIPE
+#define SLGPU_SMALL_PIPE 4
+#endif
+constexpr int kSmallPipe = SLGPU_SMALL_PIPE;  // ... in launches of at most one chunk per SIMD (f32-fast)
 #ifndef SLGPU_STAGE_OUT
 #define SLGPU_STAGE_OUT 0
 #endif
@@ -1224,10 +1228,6 @@ constexpr bool kLdsBgr = kBgrMode == 1;
 constexpr bool kTexLds = kBgrMode == 2;
 constexpr int kBgrWords = kLdsBgr ? kChunk : kTexLds ? 3 * kChunk / 4 + 4 : 4;  // u32 per wave
 
-template <int MODE>
-__device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
-                                             int total, const uint32_t* s_ent, const uint32_t* s_bgr,
-                                             float* s_sxyz, uint8_t* s_scol);
 
 // base + a 32-bit byte offset: the form global loads / stores take with an
 // SGPR base (wave-uniform pointer) and a 32-bit VGPR offset
@@ -1345,7 +1345,12 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
 
 // Phases 2-3 of a chunk (global index gc, output offset base), by one wave,
 // from the lane's loads.
-template <int MODE, int VEC>
+template <int MODE, int VEC, int PIPE>
+__device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
+                                             int total, const uint32_t* s_ent, const uint32_t* s_bgr,
+                                             float* s_sxyz, uint8_t* s_scol);
+
+template <int MODE, int VEC, int PIPE>
 __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane, const ChunkIn& in,
                                             uint32_t* s_ent, uint32_t* s_bgr, float* s_sxyz, uint8_t* s_scol) {
   const int view = static_cast<int>(gc / p.cpv);
@@ -1410,16 +1415,17 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   __builtin_amdgcn_wave_barrier();
   if (kAblate & 16) return;  // measurement only: stop after the LDS compaction
 
-  cloud_points<MODE, VEC>(p, view, cpx, base, lane, total, s_ent, s_bgr, s_sxyz, s_scol);
+  cloud_points<MODE, VEC, PIPE>(p, view, cpx, base, lane, total, s_ent, s_bgr, s_sxyz, s_scol);
 }
 
 // Phase 3 of a chunk: its `total` compacted points (s_ent: pixel | code << 10
 // | row offset << 25 on the 16-byte path, s_bgr: colour) -> xyz + BGR at
 // offset base + rank, kPipe x 64 per pass.
-template <int MODE, int VEC>
+template <int MODE, int VEC, int PIPE>
 __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
                                              int total, const uint32_t* s_ent, const uint32_t* s_bgr,
                                              float* s_sxyz, uint8_t* s_scol) {
+  constexpr int kPipe = PIPE;  // points per lane per pass
   const int mode = MODE >= 0 ? MODE : p.mode;
   const int64_t HW = p.HW;
   const bool has_tex = (mode & M_TEX) != 0;
@@ -1684,8 +1690,10 @@ __device__ __forceinline__ long long block_offset(const Params& p, int64_t b, in
   return t;
 }
 
-template <int MODE, int VEC>
-__global__ __launch_bounds__(kThreads, 5) void k_cloud(Params p) {
+// PIPE: points per lane per pass (kPipe; launches of at most one chunk per
+// SIMD take all of a chunk's points in one pass: one gather round trip)
+template <int MODE, int VEC, int PIPE = kPipe>
+__global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : 5) void k_cloud(Params p) {
   __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
   __shared__ __attribute__((aligned(16))) uint32_t s_bgr[kWaves][kBgrWords];  // colours (kBgrMode)
   __shared__ float s_sxyz[kWaves][kStageOut ? 192 : 1];      // output stage: 64 points' xyz
@@ -1710,7 +1718,7 @@ __global__ __launch_bounds__(kThreads, 5) void k_cloud(Params p) {
   if (!kCloudHoist) cloud_load<VEC>(p, gc, lane, &in);
   if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1)
     p.view_offsets[p.n_views] = base + p.chunk_counts[gc];
-  cloud_chunk<MODE, VEC>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0]);
+  cloud_chunk<MODE, VEC, PIPE>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0]);
 }
 
 }  // namespace
@@ -1922,7 +1930,8 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
   return vec ? k_decode<-1, -1, -1, 1> : k_decode<-1, -1, -1, 0>;
 }
 
-KernelFn pick_cloud(int mode, bool vec) {
+KernelFn pick_cloud(int mode, bool vec, bool small) {
+  if (vec && small && kSmallPipe > kPipe && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1, kSmallPipe>;
   if (vec && mode == M_TEX) return k_cloud<M_TEX, 1>;  // f32 xyz, pinhole rays, BGR texture
   if (vec && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1>;
   return vec ? k_cloud<-1, 1> : k_cloud<-1, 0>;
@@ -2045,7 +2054,8 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     if (cloud_mode >= 0) {
       p.mode = cloud_mode;
       void* args[] = {&p};
-      KernelFn fn = pick_cloud(cloud_mode, vec);
+      // at most one chunk per SIMD: all of a chunk's points in one pass
+      KernelFn fn = pick_cloud(cloud_mode, vec, p.n_chunks <= 4 * static_cast<int64_t>(c->n_cu));
       c->last.p[2] = p;
       c->last.fn[2] = reinterpret_cast<const void*>(fn);
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(kThreads), args, 0, s));
