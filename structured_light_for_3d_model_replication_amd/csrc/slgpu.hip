@@ -270,6 +270,39 @@ __device__ __forceinline__ long long uniform64(long long v) {
   return static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo);
 }
 
+// f64 division a / b as the compiler lowers it (v_div_scale, v_rcp_f64, two
+// Newton steps, a * r, the residual, v_div_fmas, v_div_fixup), without the
+// scale / fixup steps, which change nothing when both operands are normal
+// numbers within 2^+-300 of 1 (no rescaling, a normal quotient): the same
+// bits.  The reciprocal step depends on b only, so divisions by one b share
+// it.  div_safe(v): v is such an operand (and not +-0, whose sign the
+// residual step would lose).
+#ifndef SLGPU_DIV_SHARE
+#define SLGPU_DIV_SHARE 1
+#endif
+constexpr bool kDivShare = SLGPU_DIV_SHARE != 0;
+__device__ __forceinline__ double recip_nr(double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-b, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ double div_rn(double a, double b, double r) {
+  const double q = a * r;
+  const double e = __builtin_fma(-b, q, a);
+  return __builtin_fma(e, r, q);
+}
+__device__ __forceinline__ bool div_safe(double v) {
+  const double m = fabs(v);
+  return m >= 0x1p-300 && m <= 0x1p300;
+}
+
+// A wave-uniform double moved to SGPRs.
+__device__ __forceinline__ double uniform_f64(double v) {
+  return __longlong_as_double(uniform64(__double_as_longlong(v)));
+}
+
 __device__ __forceinline__ int wave_sum(int s) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
@@ -1437,6 +1470,13 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
   const int u_c = static_cast<int>(cpx % W);
   const int v_c = static_cast<int>(cpx / W);
   const double* pose = p.poses ? p.poses + 16 * view : nullptr;
+  // the view's pose rows, once per chunk into wave-uniform registers (read
+  // through `pose` inside the point loop they were re-loaded per point)
+  double pm[12];
+  if (pose) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) pm[k] = uniform_f64(pose[k]);
+  }
   const bool f64out = (mode & M_XYZ64) != 0;
   constexpr int dbg = kAblate;
   auto point_bgr = [&](int j, int local) -> uint32_t {
@@ -1576,19 +1616,30 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       } else {
         const double x = ra[i], y = rb[i];
         const double nrm = sqrt((x * x + y * y) + 1.0);
-        r0 = x / nrm;
-        r1 = y / nrm;
-        r2 = 1.0 / nrm;
+        // the three divisions by nrm share one reciprocal (div_rn: the
+        // compiler's own f64 division sequence, bit for bit, where it would
+        // not rescale); other operands take the operator
+        const double rn = recip_nr(nrm);
+        const bool ok = kDivShare && div_safe(x) && div_safe(y);
+        r0 = div_rn(x, nrm, rn);
+        r1 = div_rn(y, nrm, rn);
+        r2 = div_rn(1.0, nrm, rn);
+        if (!ok) {
+          r0 = x / nrm;
+          r1 = y / nrm;
+          r2 = 1.0 / nrm;
+        }
       }
       const double den = (pl[i].x * r0 + pl[i].y * r1) + pl[i].z * r2;
-      const double t = -pl[i].w / den;
+      double t = div_rn(-pl[i].w, den, recip_nr(den));
+      if (!(kDivShare && div_safe(pl[i].w) && div_safe(den))) t = -pl[i].w / den;
       X[i] = p.o0 + r0 * t;
       Y[i] = p.o1 + r1 * t;
       Z[i] = p.o2 + r2 * t;
       if (pose) {
-        const double X2 = ((pose[0] * X[i] + pose[1] * Y[i]) + pose[2] * Z[i]) + pose[3];
-        const double Y2 = ((pose[4] * X[i] + pose[5] * Y[i]) + pose[6] * Z[i]) + pose[7];
-        const double Z2 = ((pose[8] * X[i] + pose[9] * Y[i]) + pose[10] * Z[i]) + pose[11];
+        const double X2 = ((pm[0] * X[i] + pm[1] * Y[i]) + pm[2] * Z[i]) + pm[3];
+        const double Y2 = ((pm[4] * X[i] + pm[5] * Y[i]) + pm[6] * Z[i]) + pm[7];
+        const double Z2 = ((pm[8] * X[i] + pm[9] * Y[i]) + pm[10] * Z[i]) + pm[11];
         X[i] = X2;
         Y[i] = Y2;
         Z[i] = Z2;
