@@ -5,9 +5,10 @@
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 A step is one pass of the hot path over one batch of synthetic views resident
-in HBM -- k_decode (Gray decode, Gray->binary, black-plane histogram), k_count
-(adaptive-mask thresholds, mask, point/no-point decision, chunk counts),
-k_cloud (chunk offsets, ray/plane intersection, ordered stores) -- producing what the reference's
+in HBM -- k_stats (black-plane histogram, max(white - black)), k_decode (Gray
+decode, Gray->binary, adaptive-mask thresholds, mask, point/no-point decision,
+chunk counts), k_cloud (chunk offsets, ray/plane intersection, ordered
+stores) -- producing what the reference's
 gray_decode + reconstruct_point_cloud return: col_map, row_map, mask and the
 (xyz, BGR) cloud.  xyz is float32: by default SL_XYZ_F32_FAST (f32 arithmetic,
 per-coordinate relative error <= 1.02e-5 of the reference's f64, inside the
