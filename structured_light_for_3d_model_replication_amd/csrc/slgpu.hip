@@ -178,6 +178,8 @@ struct Params {
   const double* poses;
   uint16_t* codes;   // [view][HW] records: min(col, Wp-1)
   const int32_t* rec_col;  // maps + cloud on the decide path: k_cloud takes min(col, Wp-1) from this col
+  int rec12;               // cloud only on the decide path (Wp <= 4096): records packed 12 bits per pixel,
+                           // 24 B per 16 pixels (1.5 B/px written instead of 2)
                            // map and k_decode writes no records (2 B/px less k_decode write traffic)
   uint8_t* ptnib;    // [chunk][4 steps][64 lanes] point nibbles: bit e of byte (s, l) = pixel 256 s + 4 l + e
   int32_t* col_out;
@@ -892,7 +894,20 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
     for (int i = 0; i < kPx / 2; ++i)
       rec[i] = min(col[2 * i], static_cast<uint32_t>(p.Wp - 1)) |
                (min(col[2 * i + 1], static_cast<uint32_t>(p.Wp - 1)) << 16);
-    if (vec) {
+    if (vec && p.rec12) {
+      if (n_px == kPx) {  // 8 codes per 3 words, two 12-byte stores
+        uint32_t* ro = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p.codes) + 3 * o / 2);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t* r = rec + 4 * h;  // codes 8 h .. 8 h + 7, two per word
+          const uint32_t c0 = r[0] & 0xffffu, c1 = r[0] >> 16, c2 = r[1] & 0xffffu, c3 = r[1] >> 16;
+          const uint32_t c4 = r[2] & 0xffffu, c5 = r[2] >> 16, c6 = r[3] & 0xffffu, c7 = r[3] >> 16;
+          ro[3 * h] = c0 | (c1 << 12) | (c2 << 24);  // 4-byte aligned: one dwordx3 store
+          ro[3 * h + 1] = (c2 >> 8) | (c3 << 4) | (c4 << 16) | (c5 << 28);
+          ro[3 * h + 2] = (c5 >> 4) | (c6 << 8) | (c7 << 20);
+        }
+      }
+    } else if (vec) {
       if (n_px == kPx) {
         uint4* ro = reinterpret_cast<uint4*>(p.codes + o);
         ro[0] = make_uint4(rec[0], rec[1], rec[2], rec[3]);
@@ -1337,6 +1352,28 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
     }
 #pragma unroll
     for (int i = 0; i < kPx / 2; ++i) d[i] = min(c[2 * i], cmax) | (min(c[2 * i + 1], cmax) << 16);
+  } else if (vec && p.rec12) {  // 12-bit records (k_decode): 8 codes per 3 words
+    const uint2* src = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p.codes) +
+                                                      3 * (view * HW + pxl) / 2);  // 24 B, 8-byte aligned
+    uint32_t w[6];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const uint2 q = ld_side8(src + i);
+      w[2 * i] = q.x;
+      w[2 * i + 1] = q.y;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t x = w[3 * h], y = w[3 * h + 1], z = w[3 * h + 2];
+      const uint32_t c0 = x & 0xfffu, c1 = (x >> 12) & 0xfffu;
+      const uint32_t c2 = __builtin_amdgcn_alignbit(y, x, 24) & 0xfffu, c3 = (y >> 4) & 0xfffu;
+      const uint32_t c4 = (y >> 16) & 0xfffu, c5 = __builtin_amdgcn_alignbit(z, y, 28) & 0xfffu;
+      const uint32_t c6 = (z >> 8) & 0xfffu, c7 = z >> 20;
+      d[4 * h] = c0 | (c1 << 16);
+      d[4 * h + 1] = c2 | (c3 << 16);
+      d[4 * h + 2] = c4 | (c5 << 16);
+      d[4 * h + 3] = c6 | (c7 << 16);
+    }
   } else {
     const uint16_t* src = p.codes + view * HW + pxl;
     if (vec) {
@@ -1815,6 +1852,7 @@ struct sl_ctx {
   int n_cu = 0;
   bool force_3k = false;            // SLGPU_PATH=3: k_decode + k_count + k_cloud for aligned frames too (A/B)
   bool rec_from_maps = true;        // maps + cloud: k_cloud reads the col map (SLGPU_RECORDS=1: records, A/B)
+  bool rec12 = true;                // cloud only: 12-bit packed records (SLGPU_REC12=0: 16-bit, A/B)
   int prof_n = 0;
   // the last launch group's kernels and arguments (sl_time_kernels)
   // RCCL gather (sl_gather_init): communicator, this rank, count scratch
@@ -2033,6 +2071,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     p.codes = c->d_codes;
     // maps + cloud on the decide path: k_cloud reads the col map (no records)
     p.rec_col = (decide && p.col_out && cloud_mode >= 0 && c->rec_from_maps) ? p.col_out : nullptr;
+    p.rec12 = (decide && vec && !p.rec_col && cloud_mode >= 0 && p.Wp <= 4096 && c->rec12) ? 1 : 0;
     p.ptnib = c->d_ptnib;
     p.chunk_counts = c->d_chunk_counts;
     p.block_sums = c->d_block_sums;
@@ -2276,6 +2315,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
   if (per_cu > 0) c->decode_wgs = per_cu * n_cu;
   if (const char* d = getenv("SLGPU_PATH")) c->force_3k = atoi(d) == 3;
   if (const char* d = getenv("SLGPU_RECORDS")) c->rec_from_maps = atoi(d) != 1;
+  if (const char* d = getenv("SLGPU_REC12")) c->rec12 = atoi(d) != 0;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
