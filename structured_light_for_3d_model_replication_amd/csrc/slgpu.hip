@@ -295,6 +295,21 @@ __device__ __forceinline__ double div_rn(double a, double b, double r) {
   const double e = __builtin_fma(-b, q, a);
   return __builtin_fma(e, r, q);
 }
+// sqrt(s) as the compiler lowers it (v_rsq_f64, then Goldschmidt / Newton
+// steps on g ~ sqrt(s) and h ~ 1/(2 sqrt(s))) without its range scaling
+// (by 2^256 below 2^-767, undone by 2^-128) and its +-0 / inf / NaN select:
+// the same bits for s in [2^-767, 2^1000].
+__device__ __forceinline__ double sqrt_nr(double s) {
+  const double r = __builtin_amdgcn_rsq(s);
+  double g = s * r, h = r * 0.5;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  double d = __builtin_fma(-g, g, s);
+  h = __builtin_fma(h, e, h);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, s);
+  return __builtin_fma(d, h, g);
+}
 __device__ __forceinline__ bool div_safe(double v) {
   const double m = fabs(v);
   return m >= 0x1p-300 && m <= 0x1p300;
@@ -1652,12 +1667,13 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         r2 = rcz[i];
       } else {
         const double x = ra[i], y = rb[i];
-        const double nrm = sqrt((x * x + y * y) + 1.0);
+        const bool ok = kDivShare && div_safe(x) && div_safe(y);
+        const double s2 = (x * x + y * y) + 1.0;  // in [1, 2^601] when ok
+        const double nrm = ok ? sqrt_nr(s2) : sqrt(s2);
         // the three divisions by nrm share one reciprocal (div_rn: the
         // compiler's own f64 division sequence, bit for bit, where it would
         // not rescale); other operands take the operator
         const double rn = recip_nr(nrm);
-        const bool ok = kDivShare && div_safe(x) && div_safe(y);
         r0 = div_rn(x, nrm, rn);
         r1 = div_rn(y, nrm, rn);
         r2 = div_rn(1.0, nrm, rn);
