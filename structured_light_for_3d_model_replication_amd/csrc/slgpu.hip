@@ -652,6 +652,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   const float ys_early = (decide && !kDecYnLds && (mode & M_CODES) && n_px > 0)
                              ? p.yn32[static_cast<int>(px0) / p.W] : 0.0f;
   uint32_t col[kPx];
+  uint32_t pt_rec = 0xffffu;  // the lane's point bits for 12-bit records (decide path)
   if (mode & M_FROMMAPS) {
     // reconstruct_point_cloud's input col_map (clipped below, sl_system.py:626)
     const int64_t ol = view * HW + pxl;
@@ -863,7 +864,8 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         // point nibbles in k_count's layout (byte 64 s + l: pixels 256 s + 4 l + e):
         // this lane's 16 pixels are the 4 bytes at 4 lane
         const int64_t gci = static_cast<int64_t>(view) * p.cpv + civ;
-        if (live) {
+        pt_rec = pt;
+        if (live && !p.rec12) {  // (12-bit records carry the point bits: code 0xfff = no point)
           const uint32_t nw = (pt & 0xfu) | ((pt & 0xf0u) << 4) | ((pt & 0xf00u) << 8) | ((pt & 0xf000u) << 12);
           *reinterpret_cast<uint32_t*>(p.ptnib + gci * kChunkNib + 4 * lane) = nw;
         }
@@ -914,9 +916,11 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         uint32_t* ro = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p.codes) + 3 * o / 2);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const uint32_t* r = rec + 4 * h;  // codes 8 h .. 8 h + 7, two per word
-          const uint32_t c0 = r[0] & 0xffffu, c1 = r[0] >> 16, c2 = r[1] & 0xffffu, c3 = r[1] >> 16;
-          const uint32_t c4 = r[2] & 0xffffu, c5 = r[2] >> 16, c6 = r[3] & 0xffffu, c7 = r[3] >> 16;
+          const uint32_t* r = rec + 4 * h;  // codes 8 h .. 8 h + 7, two per word; 0xfff: no point
+          auto cd = [&](int k, uint32_t c) { return ((pt_rec >> (8 * h + k)) & 1u) ? c : 0xfffu; };
+          const uint32_t c0 = cd(0, r[0] & 0xffffu), c1 = cd(1, r[0] >> 16), c2 = cd(2, r[1] & 0xffffu);
+          const uint32_t c3 = cd(3, r[1] >> 16), c4 = cd(4, r[2] & 0xffffu), c5 = cd(5, r[2] >> 16);
+          const uint32_t c6 = cd(6, r[3] & 0xffffu), c7 = cd(7, r[3] >> 16);
           ro[3 * h] = c0 | (c1 << 12) | (c2 << 24);  // 4-byte aligned: one dwordx3 store
           ro[3 * h + 1] = (c2 >> 8) | (c3 << 4) | (c4 << 16) | (c5 << 28);
           ro[3 * h + 2] = (c5 >> 4) | (c6 << 8) | (c7 << 20);
@@ -1333,7 +1337,7 @@ __device__ __forceinline__ void chunk_uv(int u_c, int v_c, uint32_t e, int W, in
 struct ChunkIn {
   uint32_t d[kPx / 2];  // records (clipped column codes), 2 per word
   uint4 tq[3];          // BGR bytes of the 16 pixels (or the white plane's in tq[0])
-  uint32_t nb4;         // point nibbles of the 16 pixels
+  uint32_t ptbits;      // point bits of the 16 pixels (bit k: pixel 16 lane + k)
 };
 
 // Phase 1 of a chunk (global index gc): the lane's loads, issued by k_cloud
@@ -1368,6 +1372,7 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
 #pragma unroll
     for (int i = 0; i < kPx / 2; ++i) d[i] = min(c[2 * i], cmax) | (min(c[2 * i + 1], cmax) << 16);
   } else if (vec && p.rec12) {  // 12-bit records (k_decode): 8 codes per 3 words
+    in->ptbits = 0u;
     const uint2* src = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p.codes) +
                                                       3 * (view * HW + pxl) / 2);  // 24 B, 8-byte aligned
     uint32_t w[6];
@@ -1388,7 +1393,11 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
       d[4 * h + 1] = c2 | (c3 << 16);
       d[4 * h + 2] = c4 | (c5 << 16);
       d[4 * h + 3] = c6 | (c7 << 16);
+      const uint32_t pb = (c0 != 0xfffu) | ((c1 != 0xfffu) << 1) | ((c2 != 0xfffu) << 2) | ((c3 != 0xfffu) << 3) |
+                          ((c4 != 0xfffu) << 4) | ((c5 != 0xfffu) << 5) | ((c6 != 0xfffu) << 6) | ((c7 != 0xfffu) << 7);
+      in->ptbits |= pb << (8 * h);
     }
+    if (n_px < kPx) in->ptbits = 0u;  // lanes past the view's end (their loads read pixel 0's records)
   } else {
     const uint16_t* src = p.codes + view * HW + pxl;
     if (vec) {
@@ -1425,7 +1434,10 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
   }
   // the lane's 16 point bits (k_count): the nibbles of pixels 16 l .. 16 l + 15,
   // bytes 64 (l / 16) + 4 (l % 16) + 0..3 of the chunk
-  in->nb4 = *reinterpret_cast<const uint32_t*>(p.ptnib + gc * kChunkNib + 64 * (lane >> 4) + 4 * (lane & 15));
+  if (!(vec && p.rec12)) {
+    const uint32_t nb4 = *reinterpret_cast<const uint32_t*>(p.ptnib + gc * kChunkNib + 64 * (lane >> 4) + 4 * (lane & 15));
+    in->ptbits = (nb4 & 0xfu) | ((nb4 >> 4) & 0xf0u) | ((nb4 >> 8) & 0xf00u) | ((nb4 >> 12) & 0xf000u);
+  }
 }
 
 // Phases 2-3 of a chunk (global index gc, output offset base), by one wave,
@@ -1453,9 +1465,8 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   }
   const uint32_t* d = in.d;
   const uint4* tq = in.tq;
-  const uint32_t nb4 = in.nb4;
+  const uint32_t ptbits = in.ptbits;
   __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads come first
-  const uint32_t ptbits = (nb4 & 0xfu) | ((nb4 >> 4) & 0xf0u) | ((nb4 >> 8) & 0xf00u) | ((nb4 >> 12) & 0xf000u);
   const int n_l = __popc(ptbits);
   const int incl = wave_incl_scan(n_l, lane);
   const int total = __shfl(incl, 63, 64);
@@ -2087,7 +2098,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     p.codes = c->d_codes;
     // maps + cloud on the decide path: k_cloud reads the col map (no records)
     p.rec_col = (decide && p.col_out && cloud_mode >= 0 && c->rec_from_maps) ? p.col_out : nullptr;
-    p.rec12 = (decide && vec && !p.rec_col && cloud_mode >= 0 && p.Wp <= 4096 && c->rec12) ? 1 : 0;
+    p.rec12 = (decide && vec && !p.rec_col && cloud_mode >= 0 && p.Wp < 4096 && c->rec12) ? 1 : 0;
     p.ptnib = c->d_ptnib;
     p.chunk_counts = c->d_chunk_counts;
     p.block_sums = c->d_block_sums;
