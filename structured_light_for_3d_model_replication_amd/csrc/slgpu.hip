@@ -178,8 +178,8 @@ struct Params {
   const double* poses;
   uint16_t* codes;   // [view][HW] records: min(col, Wp-1)
   const int32_t* rec_col;  // maps + cloud on the decide path: k_cloud takes min(col, Wp-1) from this col
-  int rec12;               // cloud only on the decide path (Wp <= 4096): records packed 12 bits per pixel,
-                           // 24 B per 16 pixels (1.5 B/px written instead of 2)
+  int rec12;               // decide path (Wp < 4096): records packed 12 bits per pixel, 24 B per 16
+                           // pixels, code 0xfff = no point (1.5 B/px written, no point nibbles)
                            // map and k_decode writes no records (2 B/px less k_decode write traffic)
   uint8_t* ptnib;    // [chunk][4 steps][64 lanes] point nibbles: bit e of byte (s, l) = pixel 256 s + 4 l + e
   int32_t* col_out;
@@ -1878,7 +1878,8 @@ struct sl_ctx {
   std::vector<char> prof_decide;    // per call: M_DECIDE path (events around k_stats, k_decode, k_cloud)
   int n_cu = 0;
   bool force_3k = false;            // SLGPU_PATH=3: k_decode + k_count + k_cloud for aligned frames too (A/B)
-  bool rec_from_maps = true;        // maps + cloud: k_cloud reads the col map (SLGPU_RECORDS=1: records, A/B)
+  bool rec_from_maps = false;       // maps + cloud: k_cloud reads the col map instead of the (12-bit)
+                                    // records (SLGPU_RECORDS=0; A/B: 1.6 % slower per step at config 2)
   bool rec12 = true;                // cloud only: 12-bit packed records (SLGPU_REC12=0: 16-bit, A/B)
   int prof_n = 0;
   // the last launch group's kernels and arguments (sl_time_kernels)
@@ -2341,7 +2342,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
   c->n_cu = n_cu;
   if (per_cu > 0) c->decode_wgs = per_cu * n_cu;
   if (const char* d = getenv("SLGPU_PATH")) c->force_3k = atoi(d) == 3;
-  if (const char* d = getenv("SLGPU_RECORDS")) c->rec_from_maps = atoi(d) != 1;
+  if (const char* d = getenv("SLGPU_RECORDS")) c->rec_from_maps = atoi(d) == 0;
   if (const char* d = getenv("SLGPU_REC12")) c->rec12 = atoi(d) != 0;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
