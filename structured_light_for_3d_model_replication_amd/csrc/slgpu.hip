@@ -123,7 +123,10 @@ constexpr int M_DECIDE = 256;  // k_decode: also the mask and the |n.r| decision
 constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
 
 constexpr int kSlot = 272;                 // histogram of one view: 256 bins + max + pad (u32)
-constexpr int kHistRep = 32;               // LDS histogram replicas (one per lane of a half-wave)
+#ifndef SLGPU_HIST_REP
+#define SLGPU_HIST_REP 8
+#endif
+constexpr int kHistRep = SLGPU_HIST_REP;   // LDS histogram replicas (lane % kHistRep; 8 measured best of 1/4/8/16/32/64)
 constexpr int kHistStride = kHistRep + 1;  // bin stride: replica r of bin b sits in bank (b + r) % 32
 // Measurement-only ablations, compiled in only by -DSLGPU_ABLATE=<bits> (a
 // separate build for scripts/, never the shipped library): 1 = k_cloud without
