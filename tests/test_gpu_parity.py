@@ -460,6 +460,49 @@ def test_decode_grid_cap_outputs_identical(eng, cap, monkeypatch):
     np.testing.assert_array_equal(got[3][got[5][2]:got[5][3]], P)
 
 
+@pytest.mark.parametrize("env", [("SLGPU_PATH", "3"), ("SLGPU_RECORDS", "0"), ("SLGPU_REC12", "0")])
+def test_ab_switches_outputs_identical(eng, env, monkeypatch):
+    """The A/B switches (the three-kernel path, k_cloud reading
+    the col map, 16-bit records with point nibbles) select other kernels or
+    layouts, never other results: maps, mask, cloud and view offsets equal the
+    default engine's bit for bit on a three-view batch whose views end inside a
+    chunk (maps + cloud and cloud only; f64 and f32-fast xyz), and the last
+    view's points equal the oracle's."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 517, 1200  # HW % 16 == 0 (16-byte path), HW % 1024 != 0
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig, with_Nc=False)
+    sts, txs = zip(*[synth.render_stack(rig, seed=970 + v, view_deg=15.0 * v, device="cuda") for v in range(3)])
+    st, tx = torch.stack(sts), torch.stack(txs)
+
+    def run(e):
+        e.set_calibration(cal, H, W)
+        out = []
+        for maps in (True, False):
+            for kw in (dict(xyz_dtype=torch.float64), dict(fast_f32=True)):
+                r = e.decode_triangulate(st, texture=tx, maps=maps, cloud=True, **kw)
+                e.sync()
+                out += list(_cloud_np(r["cloud"]))
+                if maps:
+                    out += [r[k].cpu().numpy() for k in ("col_map", "row_map", "mask")]
+        return out
+
+    want = run(eng)
+    monkeypatch.setenv(*env)
+    other = core.Reconstructor(torch.device("cuda", 0))
+    try:
+        got = run(other)
+    finally:
+        other.close()
+    for a, b in zip(want, got):
+        np.testing.assert_array_equal(a, b)
+    sth, texh = sts[2].cpu().numpy(), txs[2].cpu().numpy()
+    _, _, _, P, C = o.decode_triangulate(list(sth), texh, cal)
+    off = got[2]
+    np.testing.assert_array_equal(got[0][off[2]:off[3]], P)
+    np.testing.assert_array_equal(got[1][off[2]:off[3]], C)
+
+
 @pytest.mark.parametrize("val", ["1", "2", "4", "64", "255"])
 def test_debug_env_cannot_change_results(monkeypatch, val):
     """Measurement ablations are compile-time only (-DSLGPU_ABLATE, a separate
