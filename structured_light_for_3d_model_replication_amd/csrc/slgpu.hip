@@ -63,7 +63,7 @@ constexpr int kPx = 16;                 // pixels per lane in the streaming layo
 constexpr int kChunk = 64 * kPx;        // pixels per wave (one chunk)
 constexpr int kChunkNib = kChunk / 4;   // point-nibble bytes per chunk
 #ifndef SLGPU_RING
-#define SLGPU_RING 48
+#define SLGPU_RING 40
 #endif
 constexpr int kRing = SLGPU_RING;       // stack planes in flight per lane
 #ifndef SLGPU_LOAD_AUX
