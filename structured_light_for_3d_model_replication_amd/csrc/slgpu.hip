@@ -2042,6 +2042,7 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
     if (mode == (mrch | D) && kc == 11 && kr == 11) return k_decode<11, 11, mrch | D, 1>;
     if (mode == (mrch | D) && kc == 10 && kr == 0) return k_decode<10, 0, mrch | D, 1>;
     if (mode == (mrh | D) && kc == 11 && kr == 11) return k_decode<11, 11, mrh | D, 1>;
+    if (mode == (mrh | D) && kc == 10 && kr == 0) return k_decode<10, 0, mrh | D, 1>;  // config 1 gray_decode
     if (mode == (ch | D) && kc == 11) return k_decode<11, 0, ch | D, 1>;
     if (mode == (ch | D) && kc == 10) return k_decode<10, 0, ch | D, 1>;
     if (mode == (mrc | D) && kc == 11 && kr == 11) return k_decode<11, 11, mrc | D, 1>;

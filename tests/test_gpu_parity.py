@@ -150,6 +150,24 @@ def test_synthetic_vs_oracle(eng, H, W, Wp, Hp, n_cols, n_rows, rows, mode):
             np.testing.assert_array_equal(bgr, C)
 
 
+@pytest.mark.parametrize("H,W,Wp,Hp,n_cols,n_rows,rows", [
+    (720, 1280, 1024, 768, 1024, 768, False),     # config 1 (specialised maps-only kernel)
+    (1080, 1920, 1920, 1080, 1920, 1080, True),   # 11+11 bits (specialised maps-only kernel)
+    (300, 400, 1280, 800, 1280, 800, True),       # generic kernel
+])
+def test_maps_only_vs_oracle(eng, H, W, Wp, Hp, n_cols, n_rows, rows):
+    """gray_decode's device call (maps, no cloud), which runs its own k_decode
+    instantiations: col/row maps and mask bit-exact vs the oracle."""
+    rig, st, tex, cal = _render(H, W, Wp, Hp, seed=H + 7, rows=rows)
+    sth = st.cpu().numpy()
+    col, row, mask = o.gray_decode_images(list(sth), n_cols, n_rows, o.MASK_ADAPTIVE)
+    res = eng.decode_triangulate(st, n_cols, n_rows, maps=True, cloud=False)
+    eng.sync()
+    np.testing.assert_array_equal(res["col_map"][0].cpu().numpy(), col)
+    np.testing.assert_array_equal(res["row_map"][0].cpu().numpy(), row)
+    np.testing.assert_array_equal(res["mask"][0].cpu().numpy(), mask)
+
+
 def test_full_4k_view_vs_oracle(eng):
     """Config 2 (3840x2160, 11+11 bits) at full size, bit-exact vs the oracle."""
     rig, st, tex, cal = _render(2160, 3840, 1920, 1080, seed=2)
