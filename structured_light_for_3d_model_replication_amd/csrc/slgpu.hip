@@ -2048,6 +2048,11 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
     if (mode == (mrc | D) && kc == 11 && kr == 11) return k_decode<11, 11, mrc | D, 1>;
     if (mode == (cc | D) && kc == 11) return k_decode<11, 0, cc | D, 1>;
   }
+  if (vec && (mode & M_NC) && !(mode & (M_FROMMAPS | M_PLANE_RSRC))) {  // non-pinhole rays (an Nc table)
+    constexpr int D = M_DECIDE | M_NC, mrch = M_MAPS | M_ROWS | M_CODES | M_HIST, ch = M_CODES | M_HIST;
+    if (mode == (mrch | D) && kc == 11 && kr == 11) return k_decode<11, 11, mrch | D, 1>;
+    if (mode == (ch | D) && kc == 11) return k_decode<11, 0, ch | D, 1>;
+  }
   return vec ? k_decode<-1, -1, -1, 1> : k_decode<-1, -1, -1, 0>;
 }
 

@@ -223,11 +223,15 @@ def test_non_pinhole_nc(eng):
     cal["Nc"] = Nc
     sth, texh = st.cpu().numpy(), tex.cpu().numpy()
     col, row, mask, P, C = o.decode_triangulate(list(sth), texh, cal)
-    res = _run(eng, sth, texh, cal, 1920, 1080)
-    xyz, bgr, off = _cloud_np(res["cloud"])
-    assert off[-1] == len(P)
-    np.testing.assert_array_equal(xyz.view(np.uint64), P.view(np.uint64))
-    np.testing.assert_array_equal(bgr, C)
+    for maps in (True, False):  # maps + cloud and cloud-only kernels of the Nc path
+        res = _run(eng, sth, texh, cal, 1920, 1080, maps=maps)
+        xyz, bgr, off = _cloud_np(res["cloud"])
+        assert off[-1] == len(P)
+        np.testing.assert_array_equal(xyz.view(np.uint64), P.view(np.uint64))
+        np.testing.assert_array_equal(bgr, C)
+        if maps:
+            np.testing.assert_array_equal(res["col_map"][0].cpu().numpy(), col)
+            np.testing.assert_array_equal(res["mask"][0].cpu().numpy(), mask)
 
 
 def test_repeat_calls_are_stable(eng):
