@@ -74,6 +74,10 @@ def parse(argv=None):
     ap.add_argument("--xyz", default="fast", choices=["fast", "exact"],
                     help="fast: SL_XYZ_F32_FAST (f32 arithmetic, rel err <= 1.02e-5 of the reference's f64); "
                          "exact: SL_XYZ_F32 (correctly rounded float32 of the reference's f64)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="views in flight per GPU: successive steps round-robin over this many contexts, "
+                         "each on its own HIP stream with its own outputs (one step's kernels overlap the "
+                         "next one's on the other stream)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--cpu-procs", type=int, default=None,
                     help="processes of the multi-process CPU leg (default: the core share, multi-view "
@@ -335,20 +339,35 @@ def main():
     # xyz mode is timed as a secondary
     head_fast = a.xyz == "fast" and poses is None
 
-    def step(o, maps=maps, fast=head_fast):
-        return eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
-                                      xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o)
+    def step(o, maps=maps, fast=head_fast, e=eng, stream=None):
+        return e.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
+                                    xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o, stream=stream)
 
-    for _ in range(a.warmup):
-        step(out)
-    eng.sync()
+    # --streams S: S independent contexts (own scratch, own outputs), one HIP
+    # stream each; step i runs on context i % S (S = 1: the current stream)
+    S = max(1, a.streams)
+    lanes = [(eng, out, None)]
+    for _ in range(S - 1):
+        e2 = core.Reconstructor(dev)
+        e2.set_calibration(calib, H, W)
+        e2.reserve(V, H * W)
+        lanes.append((e2, {}, torch.cuda.Stream(dev)))
+    if S > 1:
+        lanes[0] = (eng, out, torch.cuda.Stream(dev))
+
+    def run_steps(k):
+        for i in range(k):
+            e, o, st = lanes[i % S]
+            step(o, e=e, stream=st)
+
+    run_steps(max(a.warmup, S))
+    torch.cuda.synchronize(dev)
     n_pts = int(out["view_offsets"][-1].item())
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step(out)
+    run_steps(a.steps)
     torch.cuda.synchronize(dev)
     # this rank's K steps are complete here; the closing barrier's own latency
     # stays out of the interval (the max over ranks below covers rank skew)
@@ -468,7 +487,7 @@ def main():
                                    + ("col/row/mask maps + " if maps else "")
                                    + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
                        "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
-                       "parallelism": f"views sharded over {world} GPU(s)"},
+                       "parallelism": f"views sharded over {world} GPU(s)", "streams_per_gpu": S},
             "roofline": {"bound": "hbm", "scope": "whole path per step: every kernel of the step",
                          "achieved": path_gbps, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": path_gbps / HBM_PEAK_GBS, "traffic": traffic,
