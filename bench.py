@@ -42,11 +42,13 @@ CONFIGS = {
     # BASELINE.json configs.  views = views per GPU per step (weak scaling);
     # maps: also write the col/row/mask maps (what gray_decode returns); pose:
     # turntable pose epilogue (config 5's merge into one frame).
-    "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0),
+    "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0,
+               streams=6),
     "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0),
     "c3": dict(H=1080, W=1920, Wp=1920, Hp=1080, rows=True, views=36, maps=False, pose=False, deg=10.0),
     "c4": dict(H=3000, W=4000, Wp=1920, Hp=1080, rows=True, views=4, maps=False, pose=False, deg=1.0),
-    "c5": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=4, maps=False, pose=True, deg=1.0),
+    "c5": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=4, maps=False, pose=True, deg=1.0,
+               streams=2),
 }
 
 
@@ -74,8 +76,8 @@ def parse(argv=None):
     ap.add_argument("--xyz", default="fast", choices=["fast", "exact"],
                     help="fast: SL_XYZ_F32_FAST (f32 arithmetic, rel err <= 1.02e-5 of the reference's f64); "
                          "exact: SL_XYZ_F32 (correctly rounded float32 of the reference's f64)")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="views in flight per GPU: successive steps round-robin over this many contexts, "
+    ap.add_argument("--streams", type=int, default=None,
+                    help="default per config (CONFIGS: measured best, DESIGN.md 6.2); views in flight per GPU: successive steps round-robin over this many contexts, "
                          "each on its own HIP stream with its own outputs (one step's kernels overlap the "
                          "next one's on the other stream)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
@@ -339,26 +341,29 @@ def main():
     # xyz mode is timed as a secondary
     head_fast = a.xyz == "fast" and poses is None
 
-    def step(o, maps=maps, fast=head_fast, e=eng, stream=None):
-        return e.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
-                                    xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o, stream=stream)
+    def step(o, maps=maps, fast=head_fast):
+        return eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
+                                      xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o)
 
-    # --streams S: S independent contexts (own scratch, own outputs), one HIP
-    # stream each; step i runs on context i % S (S = 1: the current stream)
-    S = max(1, a.streams)
-    lanes = [(eng, out, None)]
-    for _ in range(S - 1):
-        e2 = core.Reconstructor(dev)
-        e2.set_calibration(calib, H, W)
-        e2.reserve(V, H * W)
-        lanes.append((e2, {}, torch.cuda.Stream(dev)))
+    # --streams S: core.ReconstructorPool, S contexts (own scratch, own
+    # outputs) on one HIP stream each; step i runs on lane i % S.  S = 1: the
+    # plain engine on the current stream
+    S = max(1, a.streams if a.streams is not None else cfg.get("streams", 1))
+    pool = None
     if S > 1:
-        lanes[0] = (eng, out, torch.cuda.Stream(dev))
+        pool = core.ReconstructorPool(dev, lanes=S, reuse_outputs=True)
+        pool.set_calibration(calib, H, W)
+        pool.reserve(V, H * W)
+        eng, out = pool.engines[0], pool._outs[0]
 
     def run_steps(k):
-        for i in range(k):
-            e, o, st = lanes[i % S]
-            step(o, e=e, stream=st)
+        for _ in range(k):
+            if pool is None:
+                step(out)
+            else:
+                pool.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
+                                        xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
+                                        wait_inputs=False)  # resident, never-freed inputs
 
     run_steps(max(a.warmup, S))
     torch.cuda.synchronize(dev)

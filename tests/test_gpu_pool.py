@@ -1,0 +1,90 @@
+"""ReconstructorPool (views in flight over several contexts and HIP streams):
+every call gives the single-context engine's maps, mask and cloud bit for bit,
+whatever lane it ran on, with and without reused output buffers (GPU only)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _views(n, rig, synth):
+    out = []
+    for v in range(n):
+        s, t = synth.render_stack(rig, seed=700 + v, view_deg=7.0 * v, device="cuda")
+        out.append((s.contiguous(), t.contiguous()))
+    return out
+
+
+def _host(res):
+    off = res["cloud"].offsets()
+    n = int(off[-1])
+    return (res["col_map"].cpu().numpy(), res["row_map"].cpu().numpy(), res["mask"].cpu().numpy(),
+            res["cloud"].xyz[:n].cpu().numpy(), res["cloud"].bgr[:n].cpu().numpy(), off)
+
+
+@pytest.mark.parametrize("reuse", [False, True])
+@pytest.mark.parametrize("fast", [False, True])
+def test_pool_matches_single_engine(reuse, fast):
+    from structured_light_for_3d_model_replication_amd import core, synth
+    rig = synth.Rig(H=96, W=160, Wp=256, Hp=128)
+    calib = synth.make_calibration(rig, with_Nc=False)
+    views = _views(5, rig, synth)
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(calib, rig.H, rig.W)
+    want = []
+    for s, t in views:
+        r = eng.decode_triangulate(s, rig.Wp, rig.Hp, texture=t, maps=True, cloud=True, fast_f32=fast)
+        eng.sync()
+        want.append(_host(r))
+    pool = core.ReconstructorPool(torch.device("cuda", 0), lanes=3, reuse_outputs=reuse)
+    pool.set_calibration(calib, rig.H, rig.W)
+    # every call queued before any is read: lanes overlap on the device
+    got = [pool.decode_triangulate(s, rig.Wp, rig.Hp, texture=t, maps=True, cloud=True, fast_f32=fast)
+           for s, t in views[:3]]
+    assert [r["lane"] for r in got] == [0, 1, 2]
+    for r, w in zip(got, want[:3]):
+        torch.cuda.current_stream().wait_stream(r["stream"])
+        for a, b in zip(_host(r), w):
+            np.testing.assert_array_equal(a, b)
+    # two more calls wrap onto lanes 0 and 1 (their buffers reused when asked)
+    got2 = [pool.decode_triangulate(s, rig.Wp, rig.Hp, texture=t, maps=True, cloud=True, fast_f32=fast)
+            for s, t in views[3:]]
+    assert [r["lane"] for r in got2] == [0, 1]
+    if reuse:
+        assert got2[0]["col_map"].data_ptr() == got[0]["col_map"].data_ptr()
+    pool.sync()
+    for r, w in zip(got2, want[3:]):
+        for a, b in zip(_host(r), w):
+            np.testing.assert_array_equal(a, b)
+    with pytest.raises(ValueError):
+        pool.decode_triangulate(views[0][0], rig.Wp, rig.Hp, stream=torch.cuda.current_stream())
+
+
+def test_pool_resident_inputs():
+    """wait_inputs=False on resident inputs, reused outputs: six calls
+    over two lanes in flight, each lane's last result equal to the engine's."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    rig = synth.Rig(H=120, W=200, Wp=512, Hp=256)
+    calib = synth.make_calibration(rig, with_Nc=False)
+    views = _views(2, rig, synth)
+    torch.cuda.synchronize()
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(calib, rig.H, rig.W)
+    want = []
+    for s, t in views:
+        r = eng.decode_triangulate(s, rig.Wp, rig.Hp, texture=t, maps=True, cloud=True, fast_f32=True)
+        eng.sync()
+        want.append(_host(r))
+    pool = core.ReconstructorPool(torch.device("cuda", 0), lanes=2, reuse_outputs=True)
+    pool.set_calibration(calib, rig.H, rig.W)
+    last = {}
+    for k in range(6):
+        s, t = views[k % 2]
+        last[k % 2] = pool.decode_triangulate(s, rig.Wp, rig.Hp, texture=t, maps=True, cloud=True, fast_f32=True,
+                                              wait_inputs=False)
+    pool.sync()
+    for lane in (0, 1):
+        for a, b in zip(_host(last[lane]), want[lane]):
+            np.testing.assert_array_equal(a, b)
+    pool.close()
