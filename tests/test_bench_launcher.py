@@ -44,3 +44,19 @@ def test_gpus_disagreeing_with_world_size_is_an_error():
              {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0
     assert "disagrees with WORLD_SIZE" in p.stderr
+
+
+def test_streams_defaults_per_config():
+    """--streams defaults to the per-config measured best."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    assert bench.parse([]).streams is None
+    assert bench.parse(["--streams", "3"]).streams == 3
+    assert bench.CONFIGS["c1"]["streams"] == 6 and bench.CONFIGS["c5"]["streams"] == 2
+    assert all("streams" not in bench.CONFIGS[c] for c in ("c2", "c3", "c4"))
+
+
+def test_pool_rejects_zero_lanes():
+    from structured_light_for_3d_model_replication_amd import core
+    with pytest.raises(ValueError):
+        core.ReconstructorPool(lanes=0)
