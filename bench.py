@@ -8,22 +8,36 @@ A step is one pass of the hot path over one batch of synthetic views resident
 in HBM -- k_stats (black-plane histogram, max(white - black)), k_decode (Gray
 decode, Gray->binary, adaptive-mask thresholds, mask, point/no-point decision,
 chunk counts), k_cloud (chunk offsets, ray/plane intersection, ordered
-stores) -- producing what the reference's
-gray_decode + reconstruct_point_cloud return: col_map, row_map, mask and the
-(xyz, BGR) cloud.  xyz is float32: by default SL_XYZ_F32_FAST (f32 arithmetic,
-per-coordinate relative error <= 1.02e-5 of the reference's f64, inside the
-1e-4 of BASELINE.json; --xyz exact: the correctly rounded float32 of the f64,
-f64 arithmetic); the other mode is reported beside it ("alt_xyz_mode").  Default workload = BASELINE config 2: one 3840x2160 view,
-11+11-bit column+row Gray code with inverses (46 planes), per GPU per step.
-Multi-GPU: weak scaling, views sharded over ranks with no data-path
-collective; the RCCL gather of the clouds to rank 0 is timed separately
-("gather_ms").
+stores) -- producing what the reference's gray_decode + reconstruct_point_cloud
+return: col_map, row_map, mask and the (xyz, BGR) cloud.
+
+Arithmetic: by default the triangulation is the reference's float64
+arithmetic (server/sl_system.py:614-648, same operation order, no contraction;
+xyz stored as the correctly rounded float32 of that f64: SL_XYZ_F32).
+``--xyz fast`` (SL_XYZ_F32_FAST: f32 arithmetic, per-coordinate relative
+error <= 1.02e-5) is reported beside it in "alt_xyz_mode", never as `value`.
+
+Timing: W warm-up steps, then a declared untimed pre-roll (``--preroll-ms``,
+default 300 ms of back-to-back steps, so the GPU's clocks and power state are
+at their steady state when the timed window opens -- a bench that follows an
+idle GPU would otherwise time the ramp), then exactly K steps between barrier
++ synchronize pairs, garbage collection off, one HIP event per step boundary
+on the stream (per-step min / median / max in "step_us").  Max over ranks.
+
+Default workload = BASELINE config 2: one 3840x2160 view, 11+11-bit
+column+row Gray code with inverses (46 planes), per GPU per step.
+Multi-GPU: weak scaling by default (views sharded over ranks with no
+data-path collective); the gather of the clouds to rank 0 (RCCL: torch's
+communicator, or ``--gather native`` = the library's own sl_gather) is timed
+separately and described in "multi_gpu".
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -39,22 +53,26 @@ from structured_light_for_3d_model_replication_amd import core, parallel, synth 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 CONFIGS = {
-    # BASELINE.json configs.  views = views per GPU per step (weak scaling);
-    # maps: also write the col/row/mask maps (what gray_decode returns); pose:
-    # turntable pose epilogue (config 5's merge into one frame).
+    # BASELINE.json configs.  views = views per GPU per step (weak scaling;
+    # strong: views in total); maps: also write the col/row/mask maps (what
+    # gray_decode returns); pose: turntable pose epilogue (config 5's merge
+    # into one frame).  c4 / c5: 45 views per GPU = the per-GPU share of the
+    # 360-view scan over 8 GPUs (24.8 / 17.2 GB of stacks resident in HBM);
+    # c3: the 36-view turntable scan (strong scaling shards it).
     "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0,
                streams=6),
     "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0),
     "c3": dict(H=1080, W=1920, Wp=1920, Hp=1080, rows=True, views=36, maps=False, pose=False, deg=10.0),
-    "c4": dict(H=3000, W=4000, Wp=1920, Hp=1080, rows=True, views=4, maps=False, pose=False, deg=1.0),
-    "c5": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=4, maps=False, pose=True, deg=1.0,
+    "c4": dict(H=3000, W=4000, Wp=1920, Hp=1080, rows=True, views=45, maps=False, pose=False, deg=1.0),
+    "c5": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=45, maps=False, pose=True, deg=1.0,
                streams=2),
 }
 
 
 XYZ_MODES = {True: "SL_XYZ_F32_FAST: f32 arithmetic, per-coordinate rel err <= 1.02e-5 of the reference's "
                     "f64 (tolerance 1e-4); kappa > 16 points exact",
-             False: "SL_XYZ_F32: f64 arithmetic, xyz = correctly rounded float32 of the reference's f64"}
+             False: "SL_XYZ_F32: the reference's f64 arithmetic (sl_system.py:614-648, same order, no "
+                    "contraction), xyz = correctly rounded float32 of that f64"}
 
 
 def parse(argv=None):
@@ -69,22 +87,30 @@ def parse(argv=None):
                     help="CPU plumbing test of the launcher / timing / gather (no GPU, no kernels)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--preroll-ms", dest="preroll_ms", type=float, default=300.0,
+                    help="untimed back-to-back steps after the warm-up, before the timed window (ms)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--views", type=int, default=None, help="views per GPU per step (default per config)")
     ap.add_argument("--cpu-baseline", dest="cpu_baseline", action="store_true", default=True)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
-    ap.add_argument("--xyz", default="fast", choices=["fast", "exact"],
-                    help="fast: SL_XYZ_F32_FAST (f32 arithmetic, rel err <= 1.02e-5 of the reference's f64); "
-                         "exact: SL_XYZ_F32 (correctly rounded float32 of the reference's f64)")
+    ap.add_argument("--xyz", default="exact", choices=["exact", "fast"],
+                    help="exact: SL_XYZ_F32 (the reference's f64 arithmetic, correctly rounded float32 out); "
+                         "fast: SL_XYZ_F32_FAST (f32 arithmetic, rel err <= 1.02e-5 of the reference's f64)")
     ap.add_argument("--streams", type=int, default=None,
-                    help="default per config (CONFIGS: measured best, DESIGN.md 6.2); views in flight per GPU: successive steps round-robin over this many contexts, "
-                         "each on its own HIP stream with its own outputs (one step's kernels overlap the "
-                         "next one's on the other stream)")
+                    help="default per config (CONFIGS: measured best, DESIGN.md 6.2); views in flight per GPU: "
+                         "successive steps round-robin over this many contexts, each on its own HIP stream "
+                         "with its own outputs (one step's kernels overlap the next one's on the other stream)")
+    ap.add_argument("--gather", default="torch", choices=["torch", "native"],
+                    help="N > 1: the cloud gather through torch.distributed's RCCL communicator, or the "
+                         "library's own (sl_gather_init / sl_gather_counts / sl_gather)")
+    ap.add_argument("--secondary", dest="secondary", action="store_true", default=True,
+                    help="also time the cloud-only and the other xyz mode (default on)")
+    ap.add_argument("--no-secondary", dest="secondary", action="store_false")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline sample")
     ap.add_argument("--cpu-procs", type=int, default=None,
                     help="processes of the multi-process CPU leg (default: the core share, multi-view "
                          "configs only; 0: off)")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r02_traffic_c2.json"),
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r03_traffic_c2.json"),
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
                          "scripts/traffic_from_pmc.py)")
     return ap.parse_args(argv)
@@ -121,18 +147,62 @@ def rank_env():
     return world, rank, local, distributed
 
 
+def my_views(scaling: str, V_cfg: int, world: int, rank: int) -> list[int]:
+    """Global view indices of this rank: weak = V_cfg per GPU (contiguous
+    blocks), strong = V_cfg in total sharded in contiguous blocks (view v ->
+    rank floor(v*G/V), parallel.shard_views)."""
+    if scaling == "strong":
+        return list(parallel.shard_views(V_cfg, world, rank))
+    return [rank * V_cfg + v for v in range(V_cfg)]
+
+
+def gather_report(el_s: float, n_local: int, bytes_per_point: int, device, gather_fn, distributed: bool):
+    """Multi-rank facts of the timed run, identical on every rank, for rank 0's
+    line: the communicator size torch.distributed sees, every rank's seconds
+    for the K steps and its point count; then one timed gather of the clouds
+    to rank 0 (gather_fn() -> counts as the gather's own communicator saw
+    them) with its bytes (the payload that crossed to rank 0) and GB/s."""
+    world = dist.get_world_size() if distributed else 1
+    t = torch.tensor([el_s, float(n_local)], dtype=torch.float64, device=device)
+    if distributed:
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t)
+    else:
+        outs = [t]
+    per_rank_s = [float(o[0].item()) for o in outs]
+    per_rank_pts = [int(o[1].item()) for o in outs]
+    rep = {"comm_size": world, "per_rank_s": per_rank_s, "per_rank_points": per_rank_pts}
+    if not distributed:
+        return rep
+    dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    tg = time.perf_counter()
+    counts = gather_fn()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    gt = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=device)
+    dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+    g_s = float(gt.item())
+    moved = sum(c for r, c in enumerate(counts) if r != 0) * bytes_per_point
+    rep.update({"gather_counts": [int(c) for c in counts], "gather_counts_len": len(counts),
+                "gather_bytes_to_root": int(moved), "gather_ms": 1e3 * g_s,
+                "gather_GBps": moved / g_s / 1e9 if g_s > 0 else None})
+    return rep
+
+
 def selftest(a) -> None:
     """CPU plumbing test of the multi-rank bench (``--selftest --backend gloo``):
-    the same launch, barrier + max-over-ranks timing and rank-order gather as
-    the GPU bench, with a stand-in per-rank cloud of known size instead of the
-    kernels (the kernels' parity is the GPU tests' job).  Rank 0 prints one
-    JSON line with n_gpus and the gathered point count."""
+    the same launch, barrier + max-over-ranks timing, multi-rank report and
+    rank-order gather as the GPU bench, with a stand-in per-rank cloud of
+    known size instead of the kernels (the kernels' parity is the GPU tests'
+    job).  Rank 0 prints one JSON line with n_gpus, the gathered point count
+    and the "multi_gpu" block of the GPU line."""
     world, rank, _, distributed = rank_env()
     if distributed:
         dist.init_process_group("gloo")
     V = a.views or 3
-    views = list(parallel.shard_views(V * world, world, rank)) if a.scaling == "weak" else \
-        list(parallel.shard_views(V, world, rank))
+    views = my_views(a.scaling, V, world, rank)
     n_per_view = 1000
     if distributed:
         dist.barrier()
@@ -146,16 +216,21 @@ def selftest(a) -> None:
     if distributed:
         dist.barrier()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    got = {}
+
+    def gfn():
         xa, _, counts = parallel.gather_cloud(xyz, bgr, dst=0)
-    else:
-        xa, counts = xyz, [xyz.shape[0]]
+        got["xa"] = xa
+        return counts
+    rep = gather_report(el, xyz.shape[0], 15, torch.device("cpu"), gfn, distributed)
+    xa = got.get("xa", xyz)
     if rank == 0:
         order_ok = bool(torch.equal(xa[::n_per_view, 0], torch.arange(xa.shape[0] // n_per_view,
                                                                       dtype=torch.float32)))
         print(json.dumps({"metric": "selftest", "n_gpus": world, "steps": a.steps, "scaling": a.scaling,
                           "views_total": V * world if a.scaling == "weak" else V,
-                          "gathered_points": int(xa.shape[0]), "counts": counts, "view_order_ok": order_ok,
-                          "max_rank_s": float(t.item())}))
+                          "gathered_points": int(xa.shape[0]), "counts": rep.get("gather_counts", [xyz.shape[0]]),
+                          "view_order_ok": order_ok, "max_rank_s": float(t.item()), "multi_gpu": rep}))
     if distributed:
         dist.destroy_process_group()
 
@@ -239,21 +314,41 @@ def host_info():
             "core_share": int(share) if share and share.isdigit() else None}
 
 
-def cpu_baselines(a, cfg, cfg_idx, gv, calib, rig):
-    """Rank 0, N = 1, before the GPU is touched: the oracle (a NumPy
-    restatement of the reference path, bit-exact to the fixtures the
-    reference produced; oracle/sl_oracle.py) timed on this host: 1 process,
-    and P processes for the multi-view configs (P = the box's core share)."""
+def cpu_view(cfg, cfg_idx, gv):
+    """The CPU baseline's sample view (host arrays) and its calibration."""
+    rig = synth.Rig(H=cfg["H"], W=cfg["W"], Wp=cfg["Wp"], Hp=cfg["Hp"])
     st, tx = synth.render_stack(rig, seed=1000 * cfg_idx + gv, include_rows=cfg["rows"],
                                 view_deg=cfg["deg"] * gv, device="cpu")
-    st, tx = st.numpy(), tx.numpy()
-    H, W = st.shape[1:]
+    return st.numpy(), tx.numpy(), synth.make_calibration(rig, with_Nc=False)
+
+
+def cpu_baseline_multi(a, cfg, cfg_idx):
+    """Rank 0, N = 1, BEFORE the GPU is touched (the pool forks): the oracle on
+    P processes, one view each, for the multi-view configs."""
     info = host_info()
+    procs = a.cpu_procs if a.cpu_procs else (info["core_share"] or min(os.cpu_count() or 1, 16))
+    if a.cpu_procs == 0 or procs <= 1 or not (cfg["views"] > 1 or a.cpu_procs):
+        return None
+    st, tx, calib = cpu_view(cfg, cfg_idx, 0)
+    H, W = st.shape[1:]
+    vp, np_, elp = cpu_baseline_procs(st, tx, calib, procs, a.cpu_seconds)
+    return {"value": vp, "unit": "px/s", "cores": procs, "kind": "port",
+            "sample": f"{np_} x {W}x{H} view(s) over {procs} processes (one view per process at a time), "
+                      f"{elp:.1f} s"}
+
+
+def cpu_baseline_single(a, cfg, cfg_idx, multi):
+    """Rank 0, N = 1, AFTER the GPU measurement (so that ~12 s of CPU work and
+    its garbage never sit in front of the timed window): the oracle (a NumPy
+    restatement of the reference path, bit-exact to the fixtures the reference
+    produced; oracle/sl_oracle.py) on one process."""
+    st, tx, calib = cpu_view(cfg, cfg_idx, 0)
+    H, W = st.shape[1:]
     v1, n1, el1 = cpu_baseline(st, tx, calib, a.cpu_seconds)
     out = {"value": v1, "unit": "px/s", "cores": 1, "kind": "port",
            "sample": f"{n1} x {W}x{H} view(s), {st.shape[0]} planes, oracle/sl_oracle.py "
                      f"(NumPy restatement, bit-exact to reference fixtures), 1 process, {el1:.1f} s",
-           **info}
+           **host_info()}
     # the oracle / reference speed ratio measured on one host with identical
     # outputs (scripts/ref_vs_oracle_timing.py, build container): the
     # reference's own code would run at about value / ratio here
@@ -267,13 +362,19 @@ def cpu_baselines(a, cfg, cfg_idx, gv, calib, rig):
                                          "source": f"profiles/r02_ref_vs_oracle_timing.json ({r['case']})"}
         except (OSError, ValueError, KeyError, StopIteration):
             pass
-    procs = a.cpu_procs if a.cpu_procs else (info["core_share"] or min(os.cpu_count() or 1, 16))
-    if a.cpu_procs != 0 and procs > 1 and (cfg["views"] > 1 or a.cpu_procs):
-        vp, np_, elp = cpu_baseline_procs(st, tx, calib, procs, a.cpu_seconds)
-        out["multi_process"] = {"value": vp, "unit": "px/s", "cores": procs, "kind": "port",
-                                "sample": f"{np_} x {W}x{H} view(s) over {procs} processes (one view per "
-                                          f"process at a time), {elp:.1f} s"}
+    if multi is not None:
+        out["multi_process"] = multi
     return out
+
+
+def spread(us):
+    """min / median / max (and the values, for short runs) of per-step µs."""
+    if not us:
+        return None
+    d = {"min": min(us), "median": statistics.median(us), "max": max(us), "mean": sum(us) / len(us)}
+    if len(us) <= 64:
+        d["steps"] = [round(x, 1) for x in us]
+    return d
 
 
 def main():
@@ -289,36 +390,29 @@ def main():
         return selftest(a)
     if a.backend != "nccl":
         sys.exit("bench.py: --backend gloo is only for --selftest (the GPU bench gathers over RCCL)")
-    cpu = None
-    if a.cpu_baseline and world == 1 and rank == 0:  # before this process touches the GPU (fork pool)
-        c0 = CONFIGS[a.config]
-        rig0 = synth.Rig(H=c0["H"], W=c0["W"], Wp=c0["Wp"], Hp=c0["Hp"])
-        cpu = cpu_baselines(a, c0, int(a.config[1:]), 0, synth.make_calibration(rig0, with_Nc=False), rig0)
+    cfg = CONFIGS[a.config]
+    cfg_idx = int(a.config[1:])
+    cpu_on = a.cpu_baseline and world == 1 and rank == 0
+    cpu_multi = cpu_baseline_multi(a, cfg, cfg_idx) if cpu_on else None  # forks: before the GPU
     if distributed:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local if distributed else 0)
     torch.cuda.set_device(dev)
-    cfg = CONFIGS[a.config]
     H, W, Wp, Hp, rows, maps = cfg["H"], cfg["W"], cfg["Wp"], cfg["Hp"], cfg["rows"], cfg["maps"]
     V_cfg = a.views or cfg["views"]
-    if a.scaling == "strong":
-        # the config's views in total, sharded in contiguous blocks over the ranks
-        if V_cfg < world:
-            sys.exit(f"bench.py: --scaling strong needs at least {world} views (got {V_cfg})")
-        my_views = list(parallel.shard_views(V_cfg, world, rank))
-    else:
-        my_views = [rank * V_cfg + v for v in range(V_cfg)]  # V_cfg per GPU, contiguous blocks
-    V = len(my_views)
+    if a.scaling == "strong" and V_cfg < world:
+        sys.exit(f"bench.py: --scaling strong needs at least {world} views (got {V_cfg})")
+    views = my_views(a.scaling, V_cfg, world, rank)
+    V = len(views)
     V_total = V_cfg if a.scaling == "strong" else V_cfg * world
     rig = synth.Rig(H=H, W=W, Wp=Wp, Hp=Hp)
     calib = synth.make_calibration(rig, with_Nc=False)
-    cfg_idx = int(a.config[1:])
     stack = None
     tex = torch.empty((V, H, W, 3), dtype=torch.uint8, device=dev)
     poses = torch.empty((V, 4, 4), dtype=torch.float64, device=dev) if cfg["pose"] else None
     for v in range(V):
-        gv = my_views[v]  # global view index
+        gv = views[v]  # global view index
         s, t = synth.render_stack(rig, seed=1000 * cfg_idx + gv, include_rows=rows,
                                   view_deg=cfg["deg"] * gv, device=dev)
         if stack is None:
@@ -328,6 +422,7 @@ def main():
         if poses is not None:
             poses[v].copy_(torch.from_numpy(synth.turntable_pose(cfg["deg"] * gv)))
         del s, t
+    torch.cuda.empty_cache()
     n_planes = stack.shape[1]
     nc = synth.n_bits(Wp)
     read_planes = n_planes if maps else 2 + 2 * nc
@@ -337,13 +432,14 @@ def main():
     n_cols, n_rows = Wp, (Hp if rows else 1080)
     out = {}
 
-    # SL_XYZ_F32_FAST applies without a pose (include/slgpu.h); the other
-    # xyz mode is timed as a secondary
+    # the headline xyz mode: exact (the reference's f64 arithmetic) unless
+    # --xyz fast; SL_XYZ_F32_FAST applies without a pose (include/slgpu.h)
     head_fast = a.xyz == "fast" and poses is None
 
     def step(o, maps=maps, fast=head_fast):
-        return eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
-                                      xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o)
+        eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
+                               xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o)
+        return None
 
     # --streams S: core.ReconstructorPool, S contexts (own scratch, own
     # outputs) on one HIP stream each; step i runs on lane i % S.  S = 1: the
@@ -356,36 +452,89 @@ def main():
         pool.reserve(V, H * W)
         eng, out = pool.engines[0], pool._outs[0]
 
+    cur = torch.cuda.current_stream(dev)
+
+    def one():
+        """One step; -> the stream it ran on."""
+        if pool is None:
+            step(out)
+            return cur
+        res = pool.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
+                                      xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
+                                      wait_inputs=False)  # resident inputs; outputs never read meanwhile
+        return res["stream"]
+
     def run_steps(k):
         for _ in range(k):
-            if pool is None:
-                step(out)
-            else:
-                pool.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
-                                        xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
-                                        wait_inputs=False)  # resident, never-freed inputs
+            one()
+
+    def sync_all():
+        torch.cuda.synchronize(dev)
 
     run_steps(max(a.warmup, S))
-    torch.cuda.synchronize(dev)
+    sync_all()
     n_pts = int(out["view_offsets"][-1].item())
+    # declared pre-roll: back-to-back steps until preroll_ms of wall time
+    pr_steps, t_pr = 0, time.perf_counter()
+    while (time.perf_counter() - t_pr) * 1e3 < a.preroll_ms:
+        run_steps(16)
+        sync_all()
+        pr_steps += 16
+    preroll = {"ms": 1e3 * (time.perf_counter() - t_pr), "steps": pr_steps}
+
+    def timed(k, events):
+        """K steps between barrier + synchronize pairs, gc off; with events,
+        one HIP event per step boundary on the step's stream -> (seconds,
+        per-step µs or None)."""
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(k + 1)] if events else None
+        gc.collect()
+        gc.disable()
+        try:
+            if distributed:
+                dist.barrier()
+            sync_all()
+            t0 = time.perf_counter()
+            if evs:
+                evs[0].record(cur if pool is None else pool.streams[pool._next])
+            for i in range(k):
+                st = one()
+                if evs:
+                    evs[i + 1].record(st)
+            sync_all()
+            # this rank's K steps are complete here; the closing barrier's own
+            # latency stays out of the interval (the max over ranks covers skew)
+            el = time.perf_counter() - t0
+        finally:
+            gc.enable()
+        us = [1e3 * evs[i].elapsed_time(evs[i + 1]) for i in range(k)] if evs else None
+        return el, us
+
+    el_rank, step_us = timed(a.steps, events=True)
+    t = torch.tensor([el_rank], dtype=torch.float64, device=dev)
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run_steps(a.steps)
-    torch.cuda.synchronize(dev)
-    # this rank's K steps are complete here; the closing barrier's own latency
-    # stays out of the interval (the max over ranks below covers rank skew)
-    el = time.perf_counter() - t0
-    if distributed:
-        dist.barrier()
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if distributed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
+    # control: the same K steps without the per-step events
+    el_ne, _ = timed(a.steps, events=False)
+
+    # multi-rank facts + the timed gather of the clouds to rank 0
+    n_loc = int(out["view_offsets"][-1].item())
+    if distributed and a.gather == "native":
+        def gfn():
+            _, _, counts = parallel.gather_cloud_native(eng, out["xyz"][:n_loc], out["bgr"][:n_loc], dst=0)
+            return counts
+    else:
+        def gfn():
+            _, _, counts = parallel.gather_cloud(out["xyz"][:n_loc], out["bgr"][:n_loc], dst=0)
+            return counts
+    multi = gather_report(el_rank, n_loc, 15, dev, gfn, distributed)
+    if distributed:
+        multi["gather_path"] = ("sl_gather (the library's RCCL communicator)" if a.gather == "native"
+                                else "torch.distributed batch_isend_irecv (RCCL)")
 
     # per-kernel time: HIP events recorded by the library on the launch stream
-    # around k_decode / k_count / k_cloud, in a separate pass (events between
+    # around k_stats / k_decode / k_cloud, in a separate pass (events between
     # kernels add gaps, so they stay out of the timed loop above)
     eng.profile_enable(a.steps)
     for _ in range(a.steps):
@@ -402,52 +551,38 @@ def main():
     v_last = last_px // (H * W)                 # views in the timed (last) group
     t_dec, t_cnt, t_cld = eng.time_kernels(max(a.steps, 10))
 
+    def loop_s(k, **kw):
+        o2 = {}
+        for _ in range(2):
+            step(o2, **kw)
+        sync_all()
+        t1 = time.perf_counter()
+        for _ in range(k):
+            step(o2, **kw)
+        sync_all()
+        return time.perf_counter() - t1, o2
+
     # secondary (maps configs): cloud-only mode (what generate_cloud runs: row planes unread)
     el_cloud = None
-    if maps:
-        out2 = {}
-        for _ in range(2):
-            step(out2, maps=False)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        for _ in range(a.steps):
-            step(out2, maps=False)
-        torch.cuda.synchronize(dev)
-        el_cloud = time.perf_counter() - t1
-        del out2
+    if maps and a.secondary:
+        el_cloud, o2 = loop_s(a.steps, maps=False)
+        del o2
 
-    # secondary: the other xyz mode (fast <-> correctly rounded), same workload
+    # secondary: the other xyz mode (exact <-> fast), same workload
     alt = None
-    if poses is None:
-        out3 = {}
-        for _ in range(2):
-            step(out3, fast=not head_fast)
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        for _ in range(a.steps):
-            step(out3, fast=not head_fast)
-        torch.cuda.synchronize(dev)
-        el_alt = time.perf_counter() - t1
+    if poses is None and a.secondary:
+        el_alt, o3 = loop_s(a.steps, fast=not head_fast)
         eng.profile_enable(a.steps)
         for _ in range(a.steps):
-            step(out3, fast=not head_fast)
+            step(o3, fast=not head_fast)
         _, _, acloud_ms, anl = eng.profile_read()
         eng.sync()
         alt = {"xyz_mode": XYZ_MODES[not head_fast], "px_per_s": V_total * H * W * a.steps / el_alt,
-               "ms_per_step": 1e3 * el_alt / a.steps, "k_cloud_ms": acloud_ms / max(anl, 1)}
-        del out3
+               "ms_per_step": 1e3 * el_alt / a.steps, "k_cloud_ms": acloud_ms / max(anl, 1),
+               "note": "secondary: never the headline" if not head_fast else "the reference's arithmetic"}
+        del o3
 
-    gather_ms = None
-    if distributed:
-        n_loc = int(out["view_offsets"][-1].item())
-        dist.barrier()
-        torch.cuda.synchronize(dev)
-        tg = time.perf_counter()
-        parallel.gather_cloud(out["xyz"][:n_loc], out["bgr"][:n_loc], dst=0)
-        torch.cuda.synchronize(dev)
-        gt = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=dev)
-        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
-        gather_ms = 1e3 * float(gt.item())
+    cpu = cpu_baseline_single(a, cfg, cfg_idx, cpu_multi) if cpu_on else None
 
     if rank == 0:
         px_step = V_total * H * W  # whole job: every rank's views
@@ -493,6 +628,12 @@ def main():
                                    + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
                        "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
                        "parallelism": f"views sharded over {world} GPU(s)", "streams_per_gpu": S},
+            "timing": {"preroll": preroll,
+                       "step_us": spread(step_us),
+                       "step_us_note": "HIP events at every step boundary inside the timed window, on the "
+                                       "step's stream (completion to completion)",
+                       "ms_per_step_no_events": 1e3 * el_ne / a.steps,
+                       "gc": "disabled in the timed windows"},
             "roofline": {"bound": "hbm", "scope": "whole path per step: every kernel of the step",
                          "achieved": path_gbps, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": path_gbps / HBM_PEAK_GBS, "traffic": traffic,
@@ -528,7 +669,7 @@ def main():
             "cpu_baseline": cpu,
             "points_per_view": n_pts / V,
             "cloud_only_px_per_s": None if el_cloud is None else px_step * a.steps / el_cloud,
-            "gather_ms": gather_ms,
+            "multi_gpu": multi,
             "xyz_mode": XYZ_MODES[head_fast],
             "alt_xyz_mode": alt,
         }

@@ -120,6 +120,15 @@ int sl_decode_triangulate(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_
                           uint8_t* mask_out, void* xyz_out, int xyz_dtype, uint8_t* bgr_out,
                           int64_t out_capacity, int64_t* view_offsets, void* stream);
 
+/* Masked-pixel counts (the "Processing {N} valid pixels..." line of
+ * reconstruct_point_cloud, sl_system.py:601-602: N = np.count_nonzero(mask)):
+ * arms the NEXT sl_decode_triangulate on this context (that call only; it is
+ * consumed even when the call fails) to write the number of pixels of view v
+ * that pass the mask into device_counts[v] (device int64 [n_views], 8-byte
+ * aligned), asynchronously on that call's stream.  NULL disarms.  Without it
+ * the kernels count nothing. */
+int sl_mask_counts_to(sl_ctx* ctx, int64_t* device_counts);
+
 /* reconstruct_point_cloud on caller-supplied maps (sl_system.py:584-653).
  * col_map device int32 [n_views][H][W]; mask device uint8 [n_views][H][W]
  * (non-zero = valid); tex_bgr device [n_views][H][W][3].  Outputs as above. */

@@ -125,16 +125,20 @@ class Reconstructor:
             pass
 
     # ------------------------------------------------------------ calibration
-    def set_calibration(self, calib: dict, H: int, W: int) -> None:
-        K, Oc, planes, Nc = calibration_arrays(calib, H, W)
-        # content key over every byte of the calibration (the full Nc table
-        # included: no sampling, no object identity), so a changed or reused
-        # array always re-uploads
+    @staticmethod
+    def calibration_key(calib: dict, H: int, W: int):
+        """-> (arrays, key): calibration_arrays and a content key over every
+        byte of them (the full Nc table included: no sampling, no object
+        identity), so a changed or reused array always re-uploads."""
+        K, Oc, planes, Nc = arrays = calibration_arrays(calib, H, W)
         h = _hasher()
         for a in (K, Oc, planes) + (() if Nc is None else (Nc,)):
             h.update(np.ascontiguousarray(a).view(np.uint8).reshape(-1))
             h.update(str(a.shape).encode())
-        key = (H, W, h.hexdigest(), Nc is None)
+        return arrays, (H, W, h.hexdigest(), Nc is None)
+
+    def set_calibration(self, calib: dict, H: int, W: int, *, _prepared=None) -> None:
+        (K, Oc, planes, Nc), key = _prepared if _prepared is not None else self.calibration_key(calib, H, W)
         with self._lock:
             if key == self._calib_key:
                 return
@@ -157,7 +161,7 @@ class Reconstructor:
                            texture: torch.Tensor | None = None, mask_mode: str = "adaptive",
                            maps: bool = False, cloud: bool = True, xyz_dtype=torch.float32,
                            poses: torch.Tensor | None = None, fast_f32: bool = False, stream=None,
-                           out: dict | None = None):
+                           out: dict | None = None, mask_counts: torch.Tensor | None = None):
         """Fused decode (+ triangulation) of a device stack.
 
         ``stack`` uint8 [n_img, H, W] or [V, n_img, H, W] on this device;
@@ -168,6 +172,10 @@ class Reconstructor:
         ``fast_f32`` (float32 xyz only): SL_XYZ_F32_FAST -- f32 arithmetic,
         per-coordinate relative error <= 1.02e-5 vs the reference's f64,
         instead of the correctly rounded float32 of it.
+        ``mask_counts`` (int64 [V] on this device, or None): receives each
+        view's number of pixels that pass the mask -- the N of
+        reconstruct_point_cloud's "Processing N valid pixels..." line
+        (sl_system.py:601-602) -- asynchronously, like the other outputs.
         """
         if stack.dtype != torch.uint8 or stack.device != self.device:
             raise ValueError("stack must be a uint8 tensor on the reconstructor's device")
@@ -210,9 +218,15 @@ class Reconstructor:
             bgr, vo = out["bgr"], out["view_offsets"]
             if vo.shape[0] != V + 1:
                 vo = out["view_offsets"] = torch.empty(V + 1, dtype=torch.int64, device=self.device)
+        if mask_counts is not None and (mask_counts.dtype != torch.int64 or mask_counts.device != self.device
+                                        or mask_counts.numel() < V or not mask_counts.is_contiguous()):
+            raise ValueError(f"mask_counts must be a contiguous int64 tensor of >= {V} entries on {self.device}")
         with self._lock:
             if cloud and (self._H, self._W) != (H, W):
                 raise ValueError(f"calibration is for {self._W}x{self._H}, stack is {W}x{H}")
+            if mask_counts is not None:
+                _lib.check(self._L.sl_mask_counts_to(self._ctx, mask_counts.data_ptr()), self._ctx,
+                           "sl_mask_counts_to")
             _lib.check(self._L.sl_decode_triangulate(
                 self._ctx, stack.data_ptr(), stack.stride(0), V, n_img, H, W, int(n_cols), int(n_rows),
                 _ptr(texture), 3 * H * W if texture is None else texture.stride(0), MASK_MODES[mask_mode],
@@ -396,11 +410,18 @@ class ReconstructorPool:
     maps + fast-cloud view, whose kernels already stream HBM at ~0.6 of peak.
 
     Each call's lane stream first waits for the caller's current stream (the
-    inputs are ready); the result dict carries the lane's ``"stream"`` --
+    inputs are ready, and -- with ``reuse_outputs`` -- whatever the caller
+    queued there to read that lane's previous results has run); the result
+    dict carries the lane's ``"stream"`` --
     ``torch.cuda.current_stream().wait_stream(res["stream"])`` or ``sync()``
     before reading the outputs.  With ``reuse_outputs`` each lane
     keeps its output buffers across calls (a lane's results are overwritten
-    ``lanes`` calls later), else every call allocates new ones."""
+    ``lanes`` calls later), else every call allocates new ones.
+    ``wait_inputs=False`` drops that wait: the caller then guarantees both
+    that the inputs are ready AND, with ``reuse_outputs``, that nothing still
+    queued on another stream reads the lane's previous outputs (e.g. it never
+    reads them, or it synchronised after reading them) -- the lane's kernels
+    would otherwise overwrite results a queued reader has not consumed."""
 
     def __init__(self, device=None, lanes: int = 2, reuse_outputs: bool = False):
         if lanes < 1:
@@ -418,8 +439,9 @@ class ReconstructorPool:
         return len(self.engines)
 
     def set_calibration(self, calib: dict, H: int, W: int) -> None:
+        prepared = Reconstructor.calibration_key(calib, H, W)  # hashed once for every lane
         for e in self.engines:
-            e.set_calibration(calib, H, W)
+            e.set_calibration(calib, H, W, _prepared=prepared)
 
     def reserve(self, max_views: int, max_px: int) -> None:
         for e in self.engines:

@@ -192,6 +192,8 @@ struct Params {
   uint8_t* bgr;
   int64_t* view_offsets;
   ViewStats* stats;
+  unsigned long long* masked;  // or null: += masked pixels of each view (sl_mask_counts_to; the
+                               // "Processing N valid pixels..." of sl_system.py:601-602)
   unsigned* hist;       // [view][kSlot] accumulated by this launch's k_decode
   unsigned* hist_zero;  // [view][kSlot] zeroed by this launch's k_decode (the next launch's hist)
   const int64_t* base_in;  // points of the earlier launch groups of this call, or null
@@ -571,6 +573,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   __shared__ int s_cnt[2][kWaves];
   __shared__ unsigned s_bsum[kBsSlots];  // per iteration: points (low 16 bits) + waves arrived << 16
   __shared__ uint32_t s_thr[2];          // M_DECIDE adaptive: the view's tw2, tc2
+  __shared__ unsigned s_mcount;          // M_DECIDE with p.masked: the workgroup's masked pixels
   unsigned* s_hist = s_lds;
   float4* s_pl = reinterpret_cast<float4*>(s_lds);
   float* s_xn = reinterpret_cast<float*>(s_lds) + 4 * kDecPl;
@@ -583,6 +586,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   const int64_t HW = p.HW;
   if (decide) {
     if (tid < kBsSlots) s_bsum[tid] = 0u;
+    if (tid == 0) s_mcount = 0u;  // published by the barrier of iteration 0 (or the table fill's)
     // the view's mask thresholds (k_stats' histograms), once per workgroup by
     // wave 0 while the others fill the tables: at this point no decode state
     // is live (computed inside the chunk loop they cost registers and ~9 us)
@@ -599,23 +603,30 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         }
       }
     }
-    if (kDecGlds) {
+    // The decision tables exist only for a cloud (M_CODES: the host checked
+    // the calibration against the frame and Wp <= kDecPl); a maps-only call
+    // may run on a context without calibration, or with one for another
+    // frame or a wider projector, so it loads none of them.  The fills are
+    // clamped to the LDS the tables own all the same.
+    const bool tables = (mode & M_CODES) != 0;
+    const int wp_t = min(p.Wp, kDecPl), w_t = min(p.W, kDecX);
+    if (tables && kDecGlds) {
       // the tables by LDS-DMA (16 B per lane, 1 KB per wave instruction): no
       // VGPRs, and the first chunk group's stack loads below are issued
       // while they land; the workgroup barrier before the first mask
       // (iteration 0) publishes them.  Lanes past the end repeat the last
       // entry into slack LDS (kDecPl, kDecX are multiples of 64 entries).
       typedef __attribute__((address_space(3))) void* lds_ptr_t;
-      for (int i = wid; i * 64 < p.Wp; i += kWaves)
-        __builtin_amdgcn_global_load_lds(p.planes32 + min(i * 64 + lane, p.Wp - 1), (lds_ptr_t)(s_pl + i * 64), 16, 0, 0);
-      for (int i = wid; i * 256 < p.W; i += kWaves)
-        __builtin_amdgcn_global_load_lds(p.xn32 + min(i * 256 + 4 * lane, p.W - 4), (lds_ptr_t)(s_xn + i * 256), 16, 0, 0);
-    } else {
-      for (int i = tid; i < p.Wp; i += kThreads) s_pl[i] = p.planes32[i];
-      for (int i = tid; i < p.W; i += kThreads) s_xn[i] = p.xn32[i];
+      for (int i = wid; i * 64 < wp_t; i += kWaves)
+        __builtin_amdgcn_global_load_lds(p.planes32 + min(i * 64 + lane, wp_t - 1), (lds_ptr_t)(s_pl + i * 64), 16, 0, 0);
+      for (int i = wid; i * 256 < w_t; i += kWaves)
+        __builtin_amdgcn_global_load_lds(p.xn32 + min(i * 256 + 4 * lane, w_t - 4), (lds_ptr_t)(s_xn + i * 256), 16, 0, 0);
+    } else if (tables) {
+      for (int i = tid; i < wp_t; i += kThreads) s_pl[i] = p.planes32[i];
+      for (int i = tid; i < w_t; i += kThreads) s_xn[i] = p.xn32[i];
     }
-    if (kDecYnLds)
-      for (int i = tid; i < p.H; i += kThreads) s_yn[i] = p.yn32[i];
+    if (tables && kDecYnLds)
+      for (int i = tid; i < min(p.H, kDecY); i += kThreads) s_yn[i] = p.yn32[i];
     if (!kDecGlds) __syncthreads();
   }
   uint32_t tw2 = static_cast<uint32_t>(40 + 1) * 0x00010001u;      // fixed mask:
@@ -813,6 +824,10 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
 #pragma unroll
       for (int w = 0; w < 4; ++w) ok |= mask4(word(wq, w), word(bq, w), tw2, tc2, &mb[w]) << (4 * w);
       if (n_px != kPx) ok = 0u;  // vec: whole 16-pixel groups
+      if (p.masked) {  // (uniform) the chunk's masked pixels into the workgroup's count
+        const int mc = wave_sum(__popc(ok));
+        if (lane == 0 && mc) atomicAdd(&s_mcount, static_cast<unsigned>(mc));
+      }
       if ((mode & M_MAPS) && n_px == kPx)
         *reinterpret_cast<uint4*>(p.mask_out + o) = make_uint4(mb[0], mb[1], mb[2], mb[3]);
       // ---- |n.r| > 1e-6 (sl_system.py:638-642) of the masked pixels, LDS tables ----
@@ -955,6 +970,11 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
   ++it;
   }  // chunk groups
 
+  if (decide && p.masked) {  // one global add per workgroup (its view: blockIdx.y)
+    __syncthreads();
+    if (tid == 0 && s_mcount) atomicAdd(p.masked + view, static_cast<unsigned long long>(s_mcount));
+  }
+
   if (hist) {
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) mx_acc = max(mx_acc, __shfl_xor(mx_acc, d, 64));
@@ -987,7 +1007,8 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
 // and plane gathers of nearby columns.  Every load is issued before any is
 // used (clamped, unconditional addresses).
 template <int VEC>
-__device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view, int civ, int lane, bool live) {
+__device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view, int civ, int lane, bool live,
+                                           int* masked) {
   const int mode = p.mode;
   const bool vec = VEC > 0;
   const int HW = static_cast<int>(p.HW);  // < 2^31: one view's stack is < 2 GiB
@@ -1052,6 +1073,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
     }
   }
 
+  *masked = 0;
   if (!live) return 0;
 
   // ---- thresholds (while the loads above are in flight) ----
@@ -1115,6 +1137,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
       }
     }
   }
+  if (p.masked) *masked = __popc(ok[0]) + __popc(ok[1]) + __popc(ok[2]) + __popc(ok[3]);
   if (!codes) return 0;
 
   // ---- |n.r| > 1e-6 for the masked pixels ----
@@ -1240,12 +1263,25 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
 template <int VEC>
 __global__ __launch_bounds__(kThreads, SLGPU_COUNT_WAVES) void k_count(Params p) {
   __shared__ int s_sum[kWaves];
+  __shared__ int s_msum[kWaves];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
   const int civ = blockIdx.x * kWaves + wid;
   const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
-  const int total = count_chunk<VEC>(p, gc, view, civ, lane, civ < p.cpv);
+  int mc = 0;
+  const int total = count_chunk<VEC>(p, gc, view, civ, lane, civ < p.cpv, &mc);
+  if (p.masked) {  // (uniform) the workgroup's masked pixels: one global add
+    mc = wave_sum(mc);
+    if (lane == 0) s_msum[wid] = mc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) t += s_msum[w];
+      if (t) atomicAdd(p.masked + view, static_cast<unsigned long long>(t));
+    }
+  }
   if (!(p.mode & M_CODES)) return;  // uniform: no barrier below
   if (lane == 0) s_sum[wid] = total;
   __syncthreads();
@@ -1897,6 +1933,7 @@ struct sl_ctx {
   hipEvent_t done_ev = nullptr;
   bool done_valid = false;
   int64_t last_launches = 0, last_launch_px = 0;  // sl_last_launch_info
+  int64_t* mc_next = nullptr;  // sl_mask_counts_to: the next sl_decode_triangulate's masked-pixel counts
   struct {
     bool valid = false;
     bool decide = false;  // fn[1] = k_stats (or null) instead of k_count
@@ -2082,6 +2119,8 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
   r = grow(c, &c->d_stats, &c->cap_stats, p0.n_views);
   if (r) return r;
   c->last_views = p0.n_views;
+  if (p0.masked)  // the caller's per-view counts, accumulated by the groups' k_decode / k_count
+    HIP_TRY(c, hipMemsetAsync(p0.masked, 0, sizeof(unsigned long long) * p0.n_views, s));
   hipEvent_t* ev = nullptr;
   if (!c->prof_ev.empty() && kProfEv * (c->prof_n + 1) <= static_cast<int>(c->prof_ev.size()))
     ev = &c->prof_ev[kProfEv * c->prof_n++];
@@ -2102,6 +2141,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     if (p.row_out) p.row_out += v0 * p.HW;
     if (p.mask_out) p.mask_out += v0 * p.HW;
     if (p.poses) p.poses += 16 * v0;
+    if (p.masked) p.masked += v0;
     if (p.view_offsets) p.view_offsets += v0;
     p.base_in = (v0 > 0 && p.view_offsets) ? p.view_offsets : nullptr;
     p.stats = c->d_stats + v0;
@@ -2165,6 +2205,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       void* args[] = {&p};
       KernelFn fn = pick_decode(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode, vec);
       c->last.p[0] = p;
+      c->last.p[0].masked = nullptr;  // sl_time_kernels' re-runs leave the caller's counts alone
       c->last.fn[0] = reinterpret_cast<const void*>(fn);
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dgrid, dim3(kThreads), args, 0, s));
     }
@@ -2174,6 +2215,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       void* args[] = {&p};
       const void* fn = vec ? reinterpret_cast<const void*>(k_count<1>) : reinterpret_cast<const void*>(k_count<0>);
       c->last.p[1] = p;
+      c->last.p[1].masked = nullptr;
       c->last.fn[1] = fn;
       HIP_TRY(c, hipLaunchKernel(fn, grid, dim3(kThreads), args, 0, s));
     }
@@ -2531,6 +2573,8 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
                           uint8_t* mask_out, void* xyz, int xyz_dtype, uint8_t* bgr, int64_t cap,
                           int64_t* view_offsets, void* stream) {
   if (!c) return SL_EINVAL;
+  int64_t* masked = c->mc_next;  // armed by sl_mask_counts_to for this call only (consumed even on failure)
+  c->mc_next = nullptr;
   int r = common_out_checks(c, n_views, H, W, xyz, xyz_dtype, bgr, cap, view_offsets);
   if (r) return r;
   if (!stack) return fail(c, SL_EINVAL, "stack is NULL");
@@ -2576,6 +2620,7 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   p.xyz = xyz;
   p.bgr = bgr;
   p.view_offsets = view_offsets;
+  p.masked = reinterpret_cast<unsigned long long*>(masked);
   const int nc_bit = (xyz && c->d_nc) ? M_NC : 0;
   const int hist_bit = mask_mode == SL_MASK_ADAPTIVE ? M_HIST : 0;
   const int decode_mode = (maps ? (M_MAPS | M_ROWS) : 0) | (xyz ? M_CODES : 0) | hist_bit | nc_bit | plane_rsrc;
@@ -2586,7 +2631,10 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
                    (!maps || (aligned16(col_out) && aligned16(row_out) && aligned16(mask_out)));
   // aligned frames whose f32 tables fit k_decode's LDS: mask + decision in
   // k_decode ([k_stats] + k_decode + k_cloud), else k_decode + k_count + k_cloud
-  const bool decide = vec && !c->force_3k && W <= kDecX && H <= kDecY && (!xyz || c->Wp <= kDecPl);
+  // (a maps-only call reads no calibration table: k_decode loads its tables
+  // only for a cloud, whose calibration common_out_checks matched to H x W)
+  const bool decide = vec && !c->force_3k && W <= kDecX && H <= kDecY &&
+                      (!xyz || (c->has_calib && c->W == W && c->H == H && c->Wp <= kDecPl));
   HIP_TRY(c, hipSetDevice(c->device));
   const hipStream_t s = static_cast<hipStream_t>(stream);
   r = stream_handoff(c, s);
@@ -2623,6 +2671,14 @@ int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, 
   r = stream_handoff(c, s);
   if (r) return r;
   return launch(c, p, vec, decode_mode, count_mode, cloud_mode, s);
+}
+
+int sl_mask_counts_to(sl_ctx* c, int64_t* device_counts) {
+  if (!c) return SL_EINVAL;
+  if (device_counts && (reinterpret_cast<uintptr_t>(device_counts) & 7u))
+    return fail(c, SL_EINVAL, "sl_mask_counts_to: counts must be 8-byte aligned");
+  c->mc_next = device_counts;
+  return SL_OK;
 }
 
 int sl_sync(sl_ctx* c, void* stream) {

@@ -125,7 +125,8 @@ def process_views(views, calib_data, *, n_cols=1920, n_rows=1080, device=None, w
 
 
 def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slots, keep, mask_mode="fixed",
-                      raise_errors=False, *, xyz_dtype=torch.float64, poses=None, device_sink=None, host=True):
+                      raise_errors=False, *, xyz_dtype=torch.float64, poses=None, device_sink=None, host=True,
+                      gui_log=False):
     """Views grouped by (frame size, file count), each group through one
     ``pipeline.ViewPipeline``.  ``raise_errors``: a failing folder raises
     (SLSystem.generate_clouds) instead of being logged and skipped (the batch
@@ -134,7 +135,11 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
     Device-resident use (scan360): ``device_sink(folder, xyz, bgr)`` gets each
     view's points as device tensors (valid during the call), ``poses``
     ({folder: 4x4}) are applied inside k_cloud, and ``host=False`` keeps the
-    points in HBM (no D2H, no per-view PLY, nothing in the returned dict)."""
+    points in HBM (no D2H, no per-view PLY, nothing in the returned dict).
+
+    ``gui_log`` (SLSystem.generate_clouds): each view's lines are
+    generate_cloud's (sl_system.py:574-694: decoding, "Processing N valid
+    pixels...", saving, success) instead of the batch GUI's "Saved: ..." line."""
     files = {f: io.list_stack_files(f) for f in views}
     groups: dict = {}
     for f in views:
@@ -153,7 +158,8 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
         try:
             eng.set_calibration(calib_data, H, W)
             pipe = pipeline.ViewPipeline(eng, H=H, W=W, n_img=n_img, n_cols=n_cols, n_rows=n_rows,
-                                         mask_mode=mask_mode, xyz_dtype=xyz_dtype, slots=slots)
+                                         mask_mode=mask_mode, xyz_dtype=xyz_dtype, slots=slots,
+                                         count_masked=gui_log)
         except (ValueError, IndexError) as e:
             for f in group:
                 error(f, e)
@@ -169,13 +175,22 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
                 stack[0].zero_()  # white = 0: every pixel masked out, no points
                 return True
 
-        def consume(i, xyz, bgr, group=group):
+        def consume(i, xyz, bgr, group=group, pipe=pipe):
             f = group[i]
             if f in failed:
                 return
+            path = os.path.join(f, os.path.basename(f) + ".ply")
+            if gui_log:
+                for line in ("Decoding Columns...", "Decoding Rows...", "Reconstructing 3D points...",
+                             f"Processing {pipe.masked_count(i)} valid pixels...",
+                             f"Saving {len(xyz)} points to {path}..."):
+                    log(line)
             if write:
-                save_ply(xyz, bgr, os.path.join(f, os.path.basename(f) + ".ply"))
-                log(f"Saved: {os.path.basename(f)}.ply ({len(xyz)} points)")
+                save_ply(xyz, bgr, path)
+                if gui_log:
+                    log(f"[Success] Generated {path}")
+                else:
+                    log(f"Saved: {os.path.basename(f)}.ply ({len(xyz)} points)")
             out[f] = (xyz.copy(), bgr.copy()) if keep else ([], [])
 
         def on_device(i, xyz, bgr, group=group):

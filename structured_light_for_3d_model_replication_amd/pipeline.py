@@ -109,11 +109,14 @@ class ViewPipeline:
     leave HBM -- only the 16-byte view offsets come back, to size the slices.
     ``poses`` (device or host [n_views, 4, 4] f64): view i is moved by
     ``poses[i]`` inside k_cloud (the f64 pose epilogue of decode_triangulate).
+    ``count_masked``: the kernels also count each view's masked-in pixels (the
+    N of "Processing N valid pixels...", sl_system.py:601-602);
+    ``masked_count(i)`` returns view i's inside ``consume`` / ``on_device``.
     """
 
     def __init__(self, engine: core.Reconstructor, *, H: int, W: int, n_img: int, n_cols: int = 1920,
                  n_rows: int = 1080, mask_mode: str = "adaptive", xyz_dtype=torch.float64,
-                 fast_f32: bool = False, slots: int = 3):
+                 fast_f32: bool = False, slots: int = 3, count_masked: bool = False):
         if slots < 2:
             raise ValueError("slots must be >= 2")
         self.eng = engine
@@ -137,10 +140,18 @@ class ViewPipeline:
         self._dt = [torch.empty((self.H, self.W, 3), dtype=torch.uint8, device=dev) for _ in range(slots)]
         self._hx = [torch.empty((px, 3), dtype=xyz_dtype, pin_memory=True) for _ in range(slots)]
         self._hb = [torch.empty((px, 3), dtype=torch.uint8, pin_memory=True) for _ in range(slots)]
-        self._hn = [torch.empty(2, dtype=torch.int64, pin_memory=True) for _ in range(slots)]
+        self._hn = [torch.empty(3, dtype=torch.int64, pin_memory=True) for _ in range(slots)]
+        self.count_masked = bool(count_masked)
+        self._mc = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(slots)]
+        self._masked: dict = {}
         self._out = [{} for _ in range(slots)]
         self._esz = esz
         engine.reserve(1, px)
+
+    def masked_count(self, i: int) -> int:
+        """View i's masked-in pixel count (``count_masked``), valid from its
+        ``consume`` / ``on_device`` call until ``run`` returns."""
+        return self._masked[i]
 
     def run(self, n_views: int, fill, consume=None, *, on_device=None, poses=None) -> PipelineStats:
         st = PipelineStats()
@@ -170,8 +181,12 @@ class ViewPipeline:
                     with torch.cuda.stream(self._d2h):
                         self._d2h.wait_event(done)
                         cl = self._out[k]
-                        self._hn[k].copy_(cl["view_offsets"], non_blocking=True)
+                        self._hn[k][:2].copy_(cl["view_offsets"], non_blocking=True)
+                        if self.count_masked:
+                            self._hn[k][2:].copy_(self._mc[k], non_blocking=True)
                         self._d2h.synchronize()
+                        if self.count_masked:
+                            self._masked[i] = int(self._hn[k][2])
                         n = int(self._hn[k][1] - self._hn[k][0])
                         if on_device is not None:
                             on_device(i, cl["xyz"][:n], cl["bgr"][:n])
@@ -223,7 +238,8 @@ class ViewPipeline:
                                             texture=None if gray_tex else self._dt[k], mask_mode=self.mask_mode,
                                             maps=False, cloud=True, xyz_dtype=self.xyz_dtype,
                                             poses=None if poses is None else poses[i], fast_f32=self.fast_f32,
-                                            stream=self._compute, out=self._out[k])
+                                            stream=self._compute, out=self._out[k],
+                                            mask_counts=self._mc[k] if self.count_masked else None)
                 done = torch.cuda.Event()
                 done.record(self._compute)
                 work.put((i, k, done))
@@ -235,5 +251,6 @@ class ViewPipeline:
         if err:
             raise err[0]
         self.eng.sync(self._compute)
+        self._masked.clear()
         st.wall_s = time.perf_counter() - t_start
         return st

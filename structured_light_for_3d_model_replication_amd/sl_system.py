@@ -69,22 +69,42 @@ def reconstruct_point_cloud(col_map, row_map, mask, texture, calib, *, device=No
 
 
 def decode_and_reconstruct(folder, calib, n_cols=1920, n_rows=1080, *, mask_mode="adaptive", device=None,
-                           xyz_dtype=np.float64):
+                           xyz_dtype=np.float64, count_valid=False):
     """gray_decode + reconstruct_point_cloud fused in one GPU pass (what
     generate_cloud runs).  Row planes are not read: the cloud uses only the
-    column code (sl_system.py:624-629)."""
+    column code (sl_system.py:624-629).  ``count_valid``: also return the
+    number of masked-in pixels (the kernels count them: sl_mask_counts_to)."""
     stack, texture, _ = io.read_stack(folder)
     eng = core.engine(device)
     H, W = stack.shape[1:]
     eng.set_calibration(calib, H, W)
     tdt = torch.float64 if np.dtype(xyz_dtype) == np.float64 else torch.float32
+    mc = torch.empty(1, dtype=torch.int64, device=eng.device) if count_valid else None
     res = eng.decode_triangulate(torch.from_numpy(stack).to(eng.device), n_cols, n_rows,
                                  texture=torch.from_numpy(texture).to(eng.device), mask_mode=mask_mode,
-                                 maps=False, cloud=True, xyz_dtype=tdt)
+                                 maps=False, cloud=True, xyz_dtype=tdt, mask_counts=mc)
     eng.sync()
     cloud = res["cloud"]
     n = cloud.total()
-    return cloud.xyz[:n].cpu().numpy().astype(np.float64, copy=False), cloud.bgr[:n].cpu().numpy()
+    P, C = cloud.xyz[:n].cpu().numpy().astype(np.float64, copy=False), cloud.bgr[:n].cpu().numpy()
+    return (P, C, int(mc.item())) if count_valid else (P, C)
+
+
+def index_error_stage(n_files: int, n_cols: int = 1920, n_rows: int = 1080):
+    """Where gray_decode's decode_sequence (sl_system.py:544-577) reads past
+    the last file -- the IndexError of its ``files[current_idx]`` (:553-554)
+    -- while decoding the columns ("cols"), the rows ("rows"), or never
+    (None); a short stack that simply runs out of files is not an error
+    (:550)."""
+    idx = 2
+    for stage, n in (("cols", n_cols), ("rows", n_rows)):
+        for _ in range(int(np.ceil(np.log2(n)))):
+            if idx >= n_files:
+                break
+            if idx + 1 >= n_files:
+                return stage
+            idx += 2
+    return None
 
 
 class SLSystem:
@@ -104,10 +124,21 @@ class SLSystem:
         if "Oc" not in data:
             raise ValueError("Calibration file missing 'Oc'.")
         calib = _to_numpy_calib(data)
+        # gray_decode's checks and prints, in the reference's order (:510-516,
+        # :549-554, :574-577): the stack's faults raise where it would
+        n_files = len(io.list_stack_files(scan_dir))
+        if n_files < 4:
+            raise ValueError("Not enough images in folder to decode.")
+        stage = index_error_stage(n_files)
         print("Decoding Columns...")
+        if stage == "cols":
+            raise IndexError("list index out of range")
         print("Decoding Rows...")
+        if stage == "rows":
+            raise IndexError("list index out of range")
         print("Reconstructing 3D points...")
-        points, colors = decode_and_reconstruct(scan_dir, calib, device=self.device)
+        points, colors, n_valid = decode_and_reconstruct(scan_dir, calib, device=self.device, count_valid=True)
+        print(f"Processing {n_valid} valid pixels...")
         out_path = os.path.join(scan_dir, os.path.basename(scan_dir) + ".ply")
         print(f"Saving {len(points)} points to {out_path}...")
         ply.save_ply(points, colors, out_path)
@@ -121,7 +152,10 @@ class SLSystem:
         decoding, H2D, the kernels and D2H + PLY writing of neighbouring views
         overlap.  The calibration checks and exceptions are generate_cloud's;
         a folder with fewer than 4 images raises its ValueError before any
-        view is processed.  Returns the PLY paths in ``scan_dirs`` order."""
+        view is processed.  Each view then prints generate_cloud's lines
+        ("Decoding Columns..." ... "Processing N valid pixels..." ... "[Success]
+        Generated ...") as its cloud is written.  Returns the PLY paths in
+        ``scan_dirs`` order."""
         from . import multi_point_cloud_process as mp
         if not os.path.exists(calib_file):
             raise FileNotFoundError(f"Calibration file not found at {calib_file}")
@@ -135,8 +169,5 @@ class SLSystem:
             if len(io.list_stack_files(d)) < 4:  # sl_system.py:515-516
                 raise ValueError("Not enough images in folder to decode.")
         mp._process_streamed(scan_dirs, calib, 1920, 1080, self.device, True, print, slots, False,
-                             mask_mode="adaptive", raise_errors=True)
-        outs = [os.path.join(d, os.path.basename(d) + ".ply") for d in scan_dirs]
-        for o in outs:
-            print(f"[Success] Generated {o}")
-        return outs
+                             mask_mode="adaptive", raise_errors=True, gui_log=True)
+        return [os.path.join(d, os.path.basename(d) + ".ply") for d in scan_dirs]

@@ -180,9 +180,58 @@ def cli_cases(ref, tmp):
     print("cli:", {k: v["stdout"].splitlines()[-1] for k, v in meta.items()})
 
 
+def gui_stdout_cases(ref, tmp):
+    """SLSystem.generate_cloud (server/sl_system.py:483-694, the GUI's "Generate
+    .PLY", gui.py:563) run end to end on calib.mat + an image folder, with its
+    stdout captured (folder paths as {DIR}) and the exception it raises: a full
+    46-file stack, a short 12-file stack (fewer bits), a dangling odd file in
+    the column sequence (IndexError), one in the row sequence, fewer than 4
+    files (ValueError), a missing calib file (FileNotFoundError) and a calib
+    file without 'Oc' (ValueError).  Stored: the stack, the calibration, and
+    per case the file count, stdout, exception type and message."""
+    import contextlib
+    import io as _io
+    rig, st, _ = render(36, 48, 1920, 1080, seed=25)
+    cal = synth.make_calibration(rig)
+    mat = os.path.join(tmp, "gui_calib.mat")
+    scipy.io.savemat(mat, cal)
+    mat_no_oc = os.path.join(tmp, "gui_calib_no_oc.mat")
+    scipy.io.savemat(mat_no_oc, {k: v for k, v in cal.items() if k != "Oc"})
+    cases = {"full": (46, "calib.mat"), "short": (12, "calib.mat"), "odd_cols": (9, "calib.mat"),
+             "odd_rows": (31, "calib.mat"), "three": (3, "calib.mat"), "nocalib": (46, "missing.mat"),
+             "no_oc": (46, "calib_no_oc.mat")}
+    mats = {"calib.mat": mat, "missing.mat": mat + ".missing", "calib_no_oc.mat": mat_no_oc}
+    meta = {}
+    for name, (n_files, which) in cases.items():
+        folder = os.path.join(tmp, f"gui_{name}")
+        write_stack(folder, st[:n_files], ext=".bmp")
+        buf = _io.StringIO()
+        exc = None
+        with contextlib.redirect_stdout(buf):
+            try:
+                ref["sl_generate_cloud"](None, folder, mats[which])
+            except Exception as e:  # noqa: BLE001 -- recording the reference's exception
+                exc = (type(e).__name__, str(e).replace(tmp, "{DIR}"))
+        rec = {"files": n_files, "calib": which, "stdout": buf.getvalue().replace(tmp, "{DIR}"),
+               "exception": exc}
+        ply = os.path.join(folder, os.path.basename(folder) + ".ply")
+        if os.path.exists(ply):
+            shutil.copy(ply, os.path.join(HERE, f"sl_gui_stdout_{name}.ply"))
+            rec["ply"] = f"sl_gui_stdout_{name}.ply"
+        meta[name] = rec
+    save_case("sl_gui_stdout", {"func": "gui_stdout", "cases": meta}, stack=st, **calib_arrays(cal))
+    print("gui stdout:", {k: (v["stdout"].splitlines() or [""])[-1][:60] for k, v in meta.items()})
+
+
 def main():
     ref = load_reference()
     tmp = tempfile.mkdtemp(prefix="golden_")
+    if "--only-gui-stdout" in sys.argv:
+        try:
+            gui_stdout_cases(ref, tmp)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     if "--only-cli" in sys.argv:
         try:
             cli_cases(ref, tmp)
@@ -354,6 +403,7 @@ def main():
         print("errors:", errs)
         nonzero_oc_case(ref, tmp)
         cli_cases(ref, tmp)
+        gui_stdout_cases(ref, tmp)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

@@ -149,3 +149,57 @@ def test_generate_clouds_batched_matches_generate_cloud(tmp_path):
         SLSystem().generate_clouds([dirs[0], few], mat)
     with pytest.raises(FileNotFoundError):
         SLSystem().generate_clouds(dirs, str(tmp_path / "missing.mat"))
+
+
+GUI_CASES = ["full", "short", "odd_cols", "odd_rows", "three", "nocalib", "no_oc"]
+
+
+@pytest.mark.parametrize("name", GUI_CASES)
+def test_generate_cloud_stdout_matches_the_reference(tmp_path, capsys, name):
+    """SLSystem.generate_cloud (the GUI's "Generate .PLY", gui.py:563) against
+    the reference's own generate_cloud run by tests/golden/make_golden.py
+    (sl_gui_stdout): the same stdout line for line -- including "Processing N
+    valid pixels..." (sl_system.py:602), N counted by the kernels -- the same
+    exception type and message, and the same PLY bytes."""
+    from structured_light_for_3d_model_replication_amd.sl_system import SLSystem
+    d = g.load("sl_gui_stdout")
+    case = d["meta"]["cases"][name]
+    calib = {k: v for k, v in d["calib"].items()}
+    mat = str(tmp_path / "gui_calib.mat")
+    scipy.io.savemat(mat, calib)
+    mat_no_oc = str(tmp_path / "gui_calib_no_oc.mat")
+    scipy.io.savemat(mat_no_oc, {k: v for k, v in calib.items() if k != "Oc"})
+    mats = {"calib.mat": mat, "missing.mat": mat + ".missing", "calib_no_oc.mat": mat_no_oc}
+    scan = _scan(tmp_path / f"gui_{name}", d["stack"][: case["files"]])
+    capsys.readouterr()
+    exc = None
+    try:
+        SLSystem().generate_cloud(scan, mats[case["calib"]])
+    except Exception as e:  # noqa: BLE001 -- compared with the reference's exception
+        exc = [type(e).__name__, str(e).replace(str(tmp_path), "{DIR}")]
+    assert capsys.readouterr().out.replace(str(tmp_path), "{DIR}") == case["stdout"]
+    assert exc == case["exception"]
+    ply = os.path.join(scan, os.path.basename(scan) + ".ply")
+    if "ply" in case:
+        assert open(ply).read() == g.ply_text(case["ply"])
+    else:
+        assert not os.path.exists(ply)
+
+
+def test_generate_clouds_prints_generate_clouds_lines(tmp_path, capsys):
+    """The batched generate_clouds prints, per view, generate_cloud's lines
+    with the kernels' masked-pixel count (the reference's own count for the
+    fixture stack)."""
+    from structured_light_for_3d_model_replication_amd.sl_system import SLSystem
+    d = g.load("sl_gui_stdout")
+    mat = str(tmp_path / "gui_calib.mat")
+    scipy.io.savemat(mat, d["calib"])
+    dirs = [_scan(tmp_path / f"gui_full{k}", d["stack"]) for k in range(2)]
+    capsys.readouterr()
+    SLSystem().generate_clouds(dirs, mat, slots=2)
+    out = capsys.readouterr().out
+    ref = d["meta"]["cases"]["full"]["stdout"].splitlines()
+    want = [ln for ln in ref if ln.startswith("Processing ") and "valid pixels" in ln]
+    assert want and out.count(want[0]) == 2
+    for f in dirs:
+        assert f"[Success] Generated {f}/{os.path.basename(f)}.ply" in out

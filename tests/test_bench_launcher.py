@@ -37,6 +37,14 @@ def test_gpus_n_starts_n_ranks(n, scaling, views, expect):
     assert r["gathered_points"] == expect
     assert sum(r["counts"]) == expect and len(r["counts"]) == n
     assert r["view_order_ok"]
+    # the N-GPU line's self-validating block: communicator size, every rank's
+    # timing and points, the gather's own view of the counts, bytes and rate
+    m = r["multi_gpu"]
+    assert m["comm_size"] == n and m["gather_counts_len"] == n
+    assert len(m["per_rank_s"]) == n and all(s >= 0 for s in m["per_rank_s"])
+    assert m["per_rank_points"] == m["gather_counts"] == r["counts"]
+    assert m["gather_bytes_to_root"] == 15 * (expect - r["counts"][0])
+    assert m["gather_ms"] > 0 and m["gather_GBps"] > 0
 
 
 def test_gpus_disagreeing_with_world_size_is_an_error():
@@ -54,6 +62,20 @@ def test_streams_defaults_per_config():
     assert bench.parse(["--streams", "3"]).streams == 3
     assert bench.CONFIGS["c1"]["streams"] == 6 and bench.CONFIGS["c5"]["streams"] == 2
     assert all("streams" not in bench.CONFIGS[c] for c in ("c2", "c3", "c4"))
+
+
+def test_headline_is_the_reference_arithmetic():
+    """The headline xyz mode is the reference's f64 arithmetic (sl_system.py:
+    614-648); f32-fast is only ever the secondary; a pre-roll is declared."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    a = bench.parse([])
+    assert a.xyz == "exact" and a.preroll_ms >= 100 and a.gather == "torch"
+    assert bench.parse(["--xyz", "fast"]).xyz == "fast"
+    assert bench.CONFIGS["c4"]["views"] == 45 and bench.CONFIGS["c5"]["views"] == 45
+    assert bench.CONFIGS["c3"]["views"] == 36
+    s = bench.spread([3.0, 1.0, 2.0])
+    assert s["min"] == 1.0 and s["median"] == 2.0 and s["max"] == 3.0 and s["steps"] == [3.0, 1.0, 2.0]
 
 
 def test_pool_rejects_zero_lanes():
