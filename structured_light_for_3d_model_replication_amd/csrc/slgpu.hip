@@ -1702,44 +1702,88 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       pl[i] = p.planes[c];
     }
     double X[kPipe], Y[kPipe], Z[kPipe];
+    // The kPipe points' chains (sqrt, shared reciprocal, divisions) carry no
+    // branch, so the compiler interleaves them: a point whose operands leave
+    // the range where the shortened sequences are bit-identical to the
+    // operators (div_safe) only sets its bit in `slow`, and is recomputed
+    // with the operators after the loop (a branch the wave skips when no
+    // lane needs it).  With a branch per point the chains ran one after the
+    // other, each one's full f64 latency exposed.
+    uint32_t slow = 0u;
+    // stage by stage over the kPipe points (the source order the scheduler
+    // keeps): independent instructions of different points sit side by side
+    double r0[kPipe], r1[kPipe], r2[kPipe];
+    if (mode & M_NC) {
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
+        r0[i] = ra[i];
+        r1[i] = rb[i];
+        r2[i] = rcz[i];
+      }
+    } else {
+      double nrm[kPipe], rn[kPipe];
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
+        const double x = ra[i], y = rb[i];
+        nrm[i] = sqrt_nr((x * x + y * y) + 1.0);  // s2 in [1, 2^601] when div_safe(x), div_safe(y)
+        if (!(kDivShare && div_safe(x) && div_safe(y))) slow |= 1u << i;
+      }
+      // the three divisions by nrm share one reciprocal (div_rn: the
+      // compiler's own f64 division sequence, bit for bit, where it would
+      // not rescale)
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) rn[i] = recip_nr(nrm[i]);
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
+        r0[i] = div_rn(ra[i], nrm[i], rn[i]);
+        r1[i] = div_rn(rb[i], nrm[i], rn[i]);
+        r2[i] = div_rn(1.0, nrm[i], rn[i]);
+      }
+    }
+    double den[kPipe], t[kPipe];
+#pragma unroll
+    for (int i = 0; i < kPipe; ++i) den[i] = (pl[i].x * r0[i] + pl[i].y * r1[i]) + pl[i].z * r2[i];
 #pragma unroll
     for (int i = 0; i < kPipe; ++i) {
+      t[i] = div_rn(-pl[i].w, den[i], recip_nr(den[i]));
+      if (!(kDivShare && div_safe(pl[i].w) && div_safe(den[i]))) slow |= 1u << i;
+    }
+#pragma unroll
+    for (int i = 0; i < kPipe; ++i) {
+      X[i] = p.o0 + r0[i] * t[i];
+      Y[i] = p.o1 + r1[i] * t[i];
+      Z[i] = p.o2 + r2[i] * t[i];
       if (dbg & 1) {
         X[i] = ra[i];
         Y[i] = rb[i];
         Z[i] = pl[i].w;
-        continue;
       }
-      double r0, r1, r2;
-      if (mode & M_NC) {
-        r0 = ra[i];
-        r1 = rb[i];
-        r2 = rcz[i];
-      } else {
-        const double x = ra[i], y = rb[i];
-        const bool ok = kDivShare && div_safe(x) && div_safe(y);
-        const double s2 = (x * x + y * y) + 1.0;  // in [1, 2^601] when ok
-        const double nrm = ok ? sqrt_nr(s2) : sqrt(s2);
-        // the three divisions by nrm share one reciprocal (div_rn: the
-        // compiler's own f64 division sequence, bit for bit, where it would
-        // not rescale); other operands take the operator
-        const double rn = recip_nr(nrm);
-        r0 = div_rn(x, nrm, rn);
-        r1 = div_rn(y, nrm, rn);
-        r2 = div_rn(1.0, nrm, rn);
-        if (!ok) {
+    }
+    if (slow) {  // rare: the operators' own sequences (rescaling, +-0, inf / NaN)
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
+        if (!((slow >> i) & 1u)) continue;
+        double r0, r1, r2;
+        if (mode & M_NC) {
+          r0 = ra[i];
+          r1 = rb[i];
+          r2 = rcz[i];
+        } else {
+          const double x = ra[i], y = rb[i];
+          const double nrm = sqrt((x * x + y * y) + 1.0);
           r0 = x / nrm;
           r1 = y / nrm;
           r2 = 1.0 / nrm;
         }
+        const double t = -pl[i].w / ((pl[i].x * r0 + pl[i].y * r1) + pl[i].z * r2);
+        X[i] = p.o0 + r0 * t;
+        Y[i] = p.o1 + r1 * t;
+        Z[i] = p.o2 + r2 * t;
       }
-      const double den = (pl[i].x * r0 + pl[i].y * r1) + pl[i].z * r2;
-      double t = div_rn(-pl[i].w, den, recip_nr(den));
-      if (!(kDivShare && div_safe(pl[i].w) && div_safe(den))) t = -pl[i].w / den;
-      X[i] = p.o0 + r0 * t;
-      Y[i] = p.o1 + r1 * t;
-      Z[i] = p.o2 + r2 * t;
-      if (pose) {
+    }
+    if (pose) {
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
         const double X2 = ((pm[0] * X[i] + pm[1] * Y[i]) + pm[2] * Z[i]) + pm[3];
         const double Y2 = ((pm[4] * X[i] + pm[5] * Y[i]) + pm[6] * Z[i]) + pm[7];
         const double Z2 = ((pm[8] * X[i] + pm[9] * Y[i]) + pm[10] * Z[i]) + pm[11];
@@ -1846,8 +1890,15 @@ __device__ __forceinline__ long long block_offset(const Params& p, int64_t b, in
 
 // PIPE: points per lane per pass (kPipe; launches of at most one chunk per
 // SIMD take all of a chunk's points in one pass: one gather round trip)
+#ifndef SLGPU_CLOUD_WAVES
+#define SLGPU_CLOUD_WAVES 5
+#endif
+#ifndef SLGPU_EXACT_PIPE
+#define SLGPU_EXACT_PIPE 4
+#endif
+constexpr int kExactPipe = SLGPU_EXACT_PIPE;  // points per lane per pass of the exact (f64) k_cloud<M_TEX>
 template <int MODE, int VEC, int PIPE = kPipe>
-__global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : 5) void k_cloud(Params p) {
+__global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : SLGPU_CLOUD_WAVES) void k_cloud(Params p) {
   __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
   __shared__ __attribute__((aligned(16))) uint32_t s_bgr[kWaves][kBgrWords];  // colours (kBgrMode)
   __shared__ float s_sxyz[kWaves][kStageOut ? 192 : 1];      // output stage: 64 points' xyz
@@ -2095,7 +2146,7 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
 
 KernelFn pick_cloud(int mode, bool vec, bool small) {
   if (vec && small && kSmallPipe > kPipe && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1, kSmallPipe>;
-  if (vec && mode == M_TEX) return k_cloud<M_TEX, 1>;  // f32 xyz, pinhole rays, BGR texture
+  if (vec && mode == M_TEX) return k_cloud<M_TEX, 1, kExactPipe>;  // f32 xyz, pinhole rays, BGR texture
   if (vec && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1>;
   return vec ? k_cloud<-1, 1> : k_cloud<-1, 0>;
 }
