@@ -235,6 +235,25 @@ int sl_transform_points(sl_ctx* ctx, double* xyz, int64_t n, const double* pose,
 int sl_estimate_normals(sl_ctx* ctx, const double* xyz, int64_t n, double radius, int max_nn, double* normals,
                         void* stream);
 
+/* registration_icp(source, target, max_distance, init,
+ * TransformationEstimationPointToPlane()) of merge_pro_360 (processing.py:
+ * 154-156), Open3D's RegistrationICP loop: every (moved) source point's
+ * nearest target point with ((dx^2 + dy^2) + dz^2) < max_distance^2 (least
+ * (d^2, index)); the point-to-plane step from those correspondences (JTJ and
+ * JTr folded in source order, 64-point blocks left to right; 6x6 Cholesky;
+ * update = [Rz Ry Rx | t] of the solution); transformation = update *
+ * transformation; until |d fitness| < relative_fitness and |d rmse| <
+ * relative_rmse, or max_iteration steps (Open3D's defaults: 30, 1e-6, 1e-6).
+ * source / target / target_normals: device f64 [n][3]; init and the returned
+ * transformation: host row-major 4x4; fitness = correspondences / n_src,
+ * inlier_rmse = sqrt(sum d^2 / correspondences) of the last evaluation;
+ * *iterations = steps taken.  Blocking on `stream`.  Parity vs Open3D is
+ * unpinned (oracle/merge_oracle.py restates this arithmetic). */
+int sl_icp_point_to_plane(sl_ctx* ctx, const double* source, int64_t n_src, const double* target,
+                          const double* target_normals, int64_t n_tgt, double max_distance, const double* init,
+                          int max_iteration, double relative_fitness, double relative_rmse, double* transformation,
+                          double* fitness, double* inlier_rmse, int* iterations, void* stream);
+
 /* Release the scratch buffers the merge entry points keep pooled for `device`
  * (kept otherwise for the process's lifetime, at most 16 GiB per device);
  * the bytes released -> *released_bytes (may be NULL). */

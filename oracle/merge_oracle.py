@@ -389,3 +389,200 @@ def estimate_normals(points, radius, max_nn=30):
             n = (0.0, 0.0, 1.0)
         out[i] = n
     return out
+
+
+# ---------------------------------------------------------------- ICP ----
+# registration_icp(source_down, target_down, voxel_size, init,
+# TransformationEstimationPointToPlane()) of merge_pro_360
+# (server/processing.py:154-156) -- Open3D's RegistrationICP loop
+# (open3d/pipelines/registration/Registration.cpp) and the point-to-plane
+# step (TransformationEstimation.cpp, utility/Eigen.cpp), restated with the
+# arithmetic order csrc/slmerge.hip's sl_icp_point_to_plane fixes:
+#   - correspondence of a moved source point q: the target point of least
+#     (d2, index) with d2 = ((dx*dx) + dy*dy) + dz*dz < max_distance**2
+#     (nanoflann's strict radius test; Open3D breaks distance ties arbitrarily);
+#   - r = ((e0 n0 + e1 n1) + e2 n2), e = q - t, J = (q x n, n); JTJ (upper
+#     triangle, row-major), JTr, sum d2, count folded left to right over
+#     64-source-point blocks, then the blocks left to right (Open3D: an
+#     OpenMP reduction, order unspecified);
+#   - 6x6 Cholesky (Open3D: Eigen LDLT), identity update when not positive
+#     definite; x = (alpha, beta, gamma, tx, ty, tz) -> [Rz Ry Rx | t]
+#     (TransformVector6dToMatrix4d), products ((a0 b0 + a1 b1) + a2 b2)
+#     [+ a3 b3];
+#   - transformation = update @ transformation; the source is moved by the
+#     update each step (PointCloud::Transform, row order ((m0 x + m1 y) +
+#     m2 z) + m3); init applied first unless exactly the identity;
+#   - stop when |d fitness| < relative_fitness and |d rmse| < relative_rmse.
+# PARITY UNPINNED (no Open3D in this image): the GPU matches this restatement.
+ICP_BLOCK = 64
+
+
+def _transform(P, M):
+    x, y, z = P[:, 0], P[:, 1], P[:, 2]
+    out = np.empty_like(P)
+    for r in range(3):
+        out[:, r] = ((M[r][0] * x + M[r][1] * y) + M[r][2] * z) + M[r][3]
+    return out
+
+
+def icp_correspondences(Q, target, max_distance):
+    """-> (corr int64 [n] (-1: none), d2 f64 [n])."""
+    from scipy.spatial import cKDTree
+    T = np.asarray(target, dtype=np.float64)
+    r2 = max_distance * max_distance
+    tree = cKDTree(T)
+    corr = np.full(len(Q), -1, dtype=np.int64)
+    d2 = np.zeros(len(Q))
+    cand = tree.query_ball_point(Q, max_distance * (1.0 + 1e-9) + 1e-300)
+    for i, c in enumerate(cand):
+        if not c:
+            continue
+        c = np.asarray(sorted(c), dtype=np.int64)
+        d = Q[i] - T[c]
+        dd = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+        ok = dd < r2
+        if not ok.any():
+            continue
+        c, dd = c[ok], dd[ok]
+        k = np.lexsort((c, dd))[0]
+        corr[i] = c[k]
+        d2[i] = dd[k]
+    return corr, d2
+
+
+def icp_sums(Q, target, normals, corr, d2):
+    """The 29 folded sums (JTJ upper 21, JTr 6, sum d2, count)."""
+    T = np.asarray(target, dtype=np.float64)
+    N = np.asarray(normals, dtype=np.float64)
+    n = len(Q)
+    ok = corr >= 0
+    j = np.where(ok, corr, 0)
+    s0, s1, s2 = Q[:, 0], Q[:, 1], Q[:, 2]
+    n0, n1, n2 = N[j, 0], N[j, 1], N[j, 2]
+    e0, e1, e2 = s0 - T[j, 0], s1 - T[j, 1], s2 - T[j, 2]
+    r = (e0 * n0 + e1 * n1) + e2 * n2
+    J = [s1 * n2 - s2 * n1, s2 * n0 - s0 * n2, s0 * n1 - s1 * n0, n0, n1, n2]
+    cols = []
+    for a in range(6):
+        for c in range(a, 6):
+            cols.append(J[a] * J[c])
+    for a in range(6):
+        cols.append(J[a] * r)
+    cols.append(d2)
+    cols.append(np.ones(n))
+    C = np.stack(cols, axis=1)
+    C[~ok] = 0.0  # skipped points: adding +0.0 to an accumulator that starts at +0.0
+    nb = (n + ICP_BLOCK - 1) // ICP_BLOCK
+    pad = np.zeros((nb * ICP_BLOCK, C.shape[1]))
+    pad[:n] = C
+    part = np.cumsum(pad.reshape(nb, ICP_BLOCK, -1), axis=1)[:, -1, :]  # left fold inside each block
+    out = [0.0] * C.shape[1]
+    for b in range(nb):  # blocks left to right
+        for k in range(C.shape[1]):
+            out[k] = out[k] + float(part[b, k])
+    return out
+
+
+def _mat3(a, b):
+    return [[(a[i][0] * b[0][j] + a[i][1] * b[1][j]) + a[i][2] * b[2][j] for j in range(3)] for i in range(3)]
+
+
+def mat4(a, b):
+    """Row-major 4x4 product, ((a0 b0 + a1 b1) + a2 b2) + a3 b3."""
+    return [[((a[i][0] * b[0][j] + a[i][1] * b[1][j]) + a[i][2] * b[2][j]) + a[i][3] * b[3][j]
+             for j in range(4)] for i in range(4)]
+
+
+def icp_update(sums):
+    """JTJ x = -JTr by Cholesky -> the 4x4 update (identity if not SPD)."""
+    import math
+    A = [[0.0] * 6 for _ in range(6)]
+    k = 0
+    for a in range(6):
+        for c in range(a, 6):
+            A[a][c] = A[c][a] = sums[k]
+            k += 1
+    bb = [-sums[21 + a] for a in range(6)]
+    ident = [[1.0 if i == j else 0.0 for j in range(4)] for i in range(4)]
+    L = [[0.0] * 6 for _ in range(6)]
+    for j in range(6):
+        d = A[j][j]
+        for q in range(j):
+            d = d - L[j][q] * L[j][q]
+        if not (d > 0.0) or not math.isfinite(d):
+            return ident
+        L[j][j] = math.sqrt(d)
+        for i in range(j + 1, 6):
+            v = A[i][j]
+            for q in range(j):
+                v = v - L[i][q] * L[j][q]
+            L[i][j] = v / L[j][j]
+    y = [0.0] * 6
+    for i in range(6):
+        v = bb[i]
+        for q in range(i):
+            v = v - L[i][q] * y[q]
+        y[i] = v / L[i][i]
+    x = [0.0] * 6
+    for i in range(5, -1, -1):
+        v = y[i]
+        for q in range(i + 1, 6):
+            v = v - L[q][i] * x[q]
+        x[i] = v / L[i][i]
+    if not all(math.isfinite(v) for v in x):
+        return ident
+    ca, sa, cb, sb = math.cos(x[0]), math.sin(x[0]), math.cos(x[1]), math.sin(x[1])
+    cg, sg = math.cos(x[2]), math.sin(x[2])
+    Rx = [[1.0, 0.0, 0.0], [0.0, ca, -sa], [0.0, sa, ca]]
+    Ry = [[cb, 0.0, sb], [0.0, 1.0, 0.0], [-sb, 0.0, cb]]
+    Rz = [[cg, -sg, 0.0], [sg, cg, 0.0], [0.0, 0.0, 1.0]]
+    R = _mat3(Rz, _mat3(Ry, Rx))
+    return [R[0] + [x[3]], R[1] + [x[4]], R[2] + [x[5]], [0.0, 0.0, 0.0, 1.0]]
+
+
+def registration_icp_point_to_plane(source, target, target_normals, max_distance, init=None, max_iteration=30,
+                                    relative_fitness=1e-6, relative_rmse=1e-6):
+    """-> dict(transformation 4x4 (numpy), fitness, inlier_rmse, iterations)."""
+    import math
+    Q = np.array(source, dtype=np.float64)
+    T = [[1.0 if i == j else 0.0 for j in range(4)] for i in range(4)] if init is None else \
+        [[float(v) for v in row] for row in np.asarray(init, dtype=np.float64).reshape(4, 4)]
+    n = len(Q)
+    res = {"fitness": 0.0, "inlier_rmse": 0.0, "iterations": 0}
+    if n == 0 or len(target) == 0:
+        res["transformation"] = np.array(T)
+        return res
+    ident = all(T[i][j] == (1.0 if i == j else 0.0) for i in range(4) for j in range(4))
+    if not ident:
+        Q = _transform(Q, T)
+
+    def evaluate(Q):
+        corr, d2 = icp_correspondences(Q, target, max_distance)
+        s = icp_sums(Q, target, target_normals, corr, d2)
+        cnt = s[28]
+        return s, cnt / n, (math.sqrt(s[27] / cnt) if cnt > 0.0 else 0.0)
+    sums, fit, rmse = evaluate(Q)
+    it_done = 0
+    for it in range(max_iteration):
+        U = icp_update(sums)
+        T = mat4(U, T)
+        Q = _transform(Q, U)
+        f0, r0 = fit, rmse
+        sums, fit, rmse = evaluate(Q)
+        it_done = it + 1
+        if abs(f0 - fit) < relative_fitness and abs(r0 - rmse) < relative_rmse:
+            break
+    return {"transformation": np.array(T), "fitness": fit, "inlier_rmse": rmse, "iterations": it_done}
+
+
+def rigid_inverse(M):
+    """[R | t]^-1 = [R^T | -(R^T t)], products ((a0 b0 + a1 b1) + a2 b2)."""
+    M = np.asarray(M, dtype=np.float64).reshape(4, 4)
+    R = M[:3, :3]
+    t = M[:3, 3]
+    out = np.zeros((4, 4))
+    out[:3, :3] = R.T
+    for i in range(3):
+        out[i, 3] = -((R[0, i] * t[0] + R[1, i] * t[1]) + R[2, i] * t[2])
+    out[3, 3] = 1.0
+    return out

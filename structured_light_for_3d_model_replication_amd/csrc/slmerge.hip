@@ -1199,6 +1199,103 @@ __global__ __launch_bounds__(kT) void k_fill_up(double* out, int64_t n) {
   out[3 * i + 2] = 1.0;
 }
 
+// ------------------------------------------------------------------- ICP ----
+// registration_icp(source_down, target_down, voxel_size, init,
+// TransformationEstimationPointToPlane()) of merge_pro_360
+// (processing.py:154-156), Open3D's loop (Registration.cpp RegistrationICP):
+// correspondences = each (moved) source point's nearest target point within
+// max_distance; the point-to-plane Gauss-Newton step from them; repeated
+// until fitness and inlier RMSE both change by less than their relative
+// criteria (or max_iteration).  Open3D is not in this image: parity is
+// unpinned; oracle/merge_oracle.py restates this exact arithmetic.
+constexpr int kIcpBlock = 64;  // source points per fold thread
+constexpr int kIcpSums = 29;   // JTJ upper triangle (21), JTr (6), sum of d^2, correspondences
+
+// dense cell table: dense[key] = occupied-cell index (pre-filled with -1)
+__global__ __launch_bounds__(kT) void k_icp_dense(const uint64_t* ukeys, int64_t m, int32_t* dense) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (c < m) dense[ukeys[c]] = static_cast<int32_t>(c);
+}
+
+// Nearest target point of every source point q within max_distance:
+// ((dx^2 + dy^2) + dz^2) < r2 (nanoflann's strict radius test), the least
+// (d2, target index); candidates from the 27 cells (edge >= max_distance)
+// around q's cell.  -> corr[i] (target index or -1), dist2[i].
+__global__ __launch_bounds__(kT) void k_icp_corr(const double* cur, int64_t n, Grid g, const int32_t* dense,
+                                                 const uint64_t* ukeys, int64_t m, const uint32_t* ustart,
+                                                 int64_t nt, const double* sxyz, const uint32_t* sidx, double r2,
+                                                 int32_t* corr, double* dist2) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i >= n) return;
+  const double q0 = cur[3 * i], q1 = cur[3 * i + 1], q2 = cur[3 * i + 2];
+  double bd = INFINITY;
+  int64_t bi = -1;
+  const double f0 = floor((q0 - g.lo0) / g.h), f1 = floor((q1 - g.lo1) / g.h), f2 = floor((q2 - g.lo2) / g.h);
+  // a query more than a cell outside the grid (or not finite) has no candidate cell
+  if (f0 >= -1.0 && f0 <= static_cast<double>(g.nx) && f1 >= -1.0 && f1 <= static_cast<double>(g.ny) &&
+      f2 >= -1.0 && f2 <= static_cast<double>(g.nz)) {
+    const int64_t ix = static_cast<int64_t>(f0), iy = static_cast<int64_t>(f1), iz = static_cast<int64_t>(f2);
+    for (int dx = -1; dx <= 1; ++dx)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dz = -1; dz <= 1; ++dz) {
+          const int64_t a = ix + dx, b = iy + dy, d = iz + dz;
+          if (a < 0 || a >= g.nx || b < 0 || b >= g.ny || d < 0 || d >= g.nz) continue;
+          const uint64_t key = static_cast<uint64_t>((a * g.ny + b) * g.nz + d);
+          const int64_t cc = dense ? static_cast<int64_t>(dense[key]) : find_cell(ukeys, m, key);
+          if (cc < 0) continue;
+          const int64_t t1 = cc + 1 < m ? static_cast<int64_t>(ustart[cc + 1]) : nt;
+          for (int64_t t = ustart[cc]; t < t1; ++t) {
+            const double d0 = q0 - sxyz[3 * t], d1 = q1 - sxyz[3 * t + 1], d2 = q2 - sxyz[3 * t + 2];
+            const double dd = (d0 * d0 + d1 * d1) + d2 * d2;
+            if (!(dd < r2)) continue;
+            const int64_t id = sidx[t];
+            if (dd < bd || (dd == bd && id < bi)) {
+              bd = dd;
+              bi = id;
+            }
+          }
+        }
+  }
+  corr[i] = static_cast<int32_t>(bi);
+  dist2[i] = bi >= 0 ? bd : 0.0;
+}
+
+// One thread per kIcpBlock source points, in index order: the point-to-plane
+// residual r = (vs - vt) . nt and Jacobian J = (vs x nt, nt) of every
+// correspondence, folded left to right into JTJ (upper triangle, row-major),
+// JTr, the sum of d^2 and the count -> part[b][29].  (TransformationEstimation-
+// PointToPlane::ComputeTransformation with the L2 loss: weight 1.)
+__global__ __launch_bounds__(kT) void k_icp_fold(const double* cur, int64_t n, const double* tgt, const double* tn,
+                                                 const int32_t* corr, const double* dist2, double* part) {
+  const int64_t b = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  const int64_t i0 = b * kIcpBlock;
+  if (i0 >= n) return;
+  const int64_t i1 = i0 + kIcpBlock < n ? i0 + kIcpBlock : n;
+  double acc[kIcpSums];
+#pragma unroll
+  for (int k = 0; k < kIcpSums; ++k) acc[k] = 0.0;
+  for (int64_t i = i0; i < i1; ++i) {
+    const int64_t j = corr[i];
+    if (j < 0) continue;
+    const double s0 = cur[3 * i], s1 = cur[3 * i + 1], s2 = cur[3 * i + 2];
+    const double n0 = tn[3 * j], n1 = tn[3 * j + 1], n2 = tn[3 * j + 2];
+    const double e0 = s0 - tgt[3 * j], e1 = s1 - tgt[3 * j + 1], e2 = s2 - tgt[3 * j + 2];
+    const double r = (e0 * n0 + e1 * n1) + e2 * n2;
+    const double J[6] = {s1 * n2 - s2 * n1, s2 * n0 - s0 * n2, s0 * n1 - s1 * n0, n0, n1, n2};
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int c = a; c < 6; ++c) acc[k++] += J[a] * J[c];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] += J[a] * r;
+    acc[27] += dist2[i];
+    acc[28] += 1.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kIcpSums; ++k) part[kIcpSums * b + k] = acc[k];
+}
+
 // ------------------------------------------------------------------ host ----
 unsigned blocks(int64_t n) { return static_cast<unsigned>((n + kT - 1) / kT); }
 
@@ -1786,6 +1883,177 @@ int sl_estimate_normals(sl_ctx* c, const double* xyz, int64_t n, double radius, 
   MTRY(c, hipGetLastError());
   MTRY(c, hipStreamSynchronize(s));
   return SL_OK;
+}
+
+// registration_icp with TransformationEstimationPointToPlane (processing.py:
+// 154-156).  Host side of each iteration: the block partials folded left to
+// right, the 6x6 normal equations JTJ x = -JTr by Cholesky (Open3D: Eigen
+// LDLT; identity when not positive definite), x = (alpha, beta, gamma, t) ->
+// update = [Rz(gamma) Ry(beta) Rx(alpha) | t] (TransformVector6dToMatrix4d),
+// transformation = update * transformation, source moved by update.
+namespace {
+
+void icp_mat3(const double a[3][3], const double b[3][3], double o[3][3]) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) o[i][j] = (a[i][0] * b[0][j] + a[i][1] * b[1][j]) + a[i][2] * b[2][j];
+}
+
+void icp_mat4(const double* a, const double* b, double* o) {  // row-major 4x4: o = a b
+  double t[16];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j)
+      t[4 * i + j] = ((a[4 * i] * b[j] + a[4 * i + 1] * b[4 + j]) + a[4 * i + 2] * b[8 + j]) + a[4 * i + 3] * b[12 + j];
+  memcpy(o, t, sizeof(t));
+}
+
+// 6x6 JTJ x = -JTr (sums: JTJ upper triangle row-major, then JTr) -> update
+// (row-major 4x4); false (identity update) when JTJ is not positive definite
+bool icp_update(const double* sums, double* update) {
+  double A[6][6], L[6][6] = {}, y[6], x[6], bb[6];
+  int k = 0;
+  for (int a = 0; a < 6; ++a)
+    for (int c = a; c < 6; ++c, ++k) A[a][c] = A[c][a] = sums[k];
+  for (int a = 0; a < 6; ++a) bb[a] = -sums[21 + a];
+  for (int i = 0; i < 16; ++i) update[i] = (i % 5 == 0) ? 1.0 : 0.0;
+  for (int j = 0; j < 6; ++j) {
+    double d = A[j][j];
+    for (int q = 0; q < j; ++q) d = d - L[j][q] * L[j][q];
+    if (!(d > 0.0) || !std::isfinite(d)) return false;
+    L[j][j] = std::sqrt(d);
+    for (int i = j + 1; i < 6; ++i) {
+      double v = A[i][j];
+      for (int q = 0; q < j; ++q) v = v - L[i][q] * L[j][q];
+      L[i][j] = v / L[j][j];
+    }
+  }
+  for (int i = 0; i < 6; ++i) {
+    double v = bb[i];
+    for (int q = 0; q < i; ++q) v = v - L[i][q] * y[q];
+    y[i] = v / L[i][i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    double v = y[i];
+    for (int q = i + 1; q < 6; ++q) v = v - L[q][i] * x[q];
+    x[i] = v / L[i][i];
+  }
+  for (int i = 0; i < 6; ++i)
+    if (!std::isfinite(x[i])) return false;
+  const double ca = std::cos(x[0]), sa = std::sin(x[0]), cb = std::cos(x[1]), sb = std::sin(x[1]);
+  const double cg = std::cos(x[2]), sg = std::sin(x[2]);
+  const double Rx[3][3] = {{1.0, 0.0, 0.0}, {0.0, ca, -sa}, {0.0, sa, ca}};
+  const double Ry[3][3] = {{cb, 0.0, sb}, {0.0, 1.0, 0.0}, {-sb, 0.0, cb}};
+  const double Rz[3][3] = {{cg, -sg, 0.0}, {sg, cg, 0.0}, {0.0, 0.0, 1.0}};
+  double M[3][3], R[3][3];
+  icp_mat3(Ry, Rx, M);
+  icp_mat3(Rz, M, R);
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) update[4 * i + j] = R[i][j];
+    update[4 * i + 3] = x[3 + i];
+  }
+  return true;
+}
+
+}  // namespace
+
+int sl_icp_point_to_plane(sl_ctx* c, const double* source, int64_t n_src, const double* target,
+                          const double* target_normals, int64_t n_tgt, double max_distance, const double* init,
+                          int max_iteration, double relative_fitness, double relative_rmse, double* transformation,
+                          double* fitness, double* inlier_rmse, int* iterations, void* stream) {
+  if (!c || n_src < 0 || n_tgt < 0 || !init || !transformation || max_iteration < 0 ||
+      (n_src && !source) || (n_tgt && (!target || !target_normals)))
+    return SL_EINVAL;
+  if (n_src >= (1ll << 31) || n_tgt >= (1ll << 31)) return slgpu_fail(c, SL_EINVAL, "at most 2^31 - 1 points");
+  if (!(max_distance > 0.0)) return slgpu_fail(c, SL_EINVAL, "max_correspondence_distance must be > 0");
+  double T[16];
+  memcpy(T, init, sizeof(T));
+  double fit = 0.0, rmse = 0.0;
+  int iters = 0;
+  auto finish = [&]() {
+    memcpy(transformation, T, sizeof(T));
+    if (fitness) *fitness = fit;
+    if (inlier_rmse) *inlier_rmse = rmse;
+    if (iterations) *iterations = iters;
+    return SL_OK;
+  };
+  if (n_src == 0 || n_tgt == 0) return finish();
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  PoolStream pool_stream(s);
+  MTRY(c, hipSetDevice(slgpu_device(c)));
+  // the target's cell grid (cells of edge >= max_distance: the 27 around a
+  // query's cell hold its ball)
+  double bnd[6];
+  int r = bounds(c, target, n_tgt, bnd, s);
+  if (r) return r;
+  double emax = 0.0;
+  for (int k = 0; k < 3; ++k) emax = std::max(emax, bnd[3 + k] - bnd[k]);
+  if (!std::isfinite(emax)) return slgpu_fail(c, SL_EINVAL, "non-finite target coordinates");
+  Grid g;
+  if (!make_grid(bnd, bnd + 3, std::max(max_distance, emax / 1.0e6), &g))
+    return slgpu_fail(c, SL_EINVAL, "correspondence grid is too large");
+  DBuf<uint64_t> keys, ukeys;
+  DBuf<uint32_t> idx, ustart;
+  int64_t m = 0;
+  r = cells(c, target, n_tgt, g, keys, idx, ukeys, ustart, &m, s);
+  if (r) return r;
+  DBuf<double> sxyz, cur, d2, part, dmat;
+  DBuf<int32_t> corr, dense;
+  MTRY(c, sxyz.alloc(3 * n_tgt));
+  hipLaunchKernelGGL(k_gather_sorted, dim3(blocks(n_tgt)), dim3(kT), 0, s, target, idx.p, n_tgt, sxyz.p);
+  const int64_t ncell = (g.nx * g.ny) * g.nz;
+  if (ncell <= (int64_t{1} << 26)) {  // a dense cell table (<= 256 MB), else binary search
+    MTRY(c, dense.alloc(ncell));
+    MTRY(c, hipMemsetAsync(dense.p, 0xff, sizeof(int32_t) * ncell, s));
+    hipLaunchKernelGGL(k_icp_dense, dim3(blocks(m)), dim3(kT), 0, s, ukeys.p, m, dense.p);
+  }
+  const int64_t nb = (n_src + kIcpBlock - 1) / kIcpBlock;
+  MTRY(c, cur.alloc(3 * n_src));
+  MTRY(c, d2.alloc(n_src));
+  MTRY(c, corr.alloc(n_src));
+  MTRY(c, part.alloc(kIcpSums * nb));
+  MTRY(c, dmat.alloc(16));
+  MTRY(c, hipMemcpyAsync(cur.p, source, sizeof(double) * 3 * n_src, hipMemcpyDeviceToDevice, s));
+  std::vector<double> hpart(static_cast<size_t>(kIcpSums * nb));
+  double sums[kIcpSums];
+  // pcd.Transform(init) unless init is the identity (exactly)
+  bool ident = true;
+  for (int i = 0; i < 16; ++i) ident = ident && T[i] == ((i % 5 == 0) ? 1.0 : 0.0);
+  auto move = [&](const double* M) -> int {
+    MTRY(c, hipMemcpyAsync(dmat.p, M, sizeof(double) * 16, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_transform, dim3(blocks(n_src)), dim3(kT), 0, s, cur.p, n_src, dmat.p);
+    MTRY(c, hipGetLastError());
+    MTRY(c, hipStreamSynchronize(s));  // dmat (device) and M (host) are reused
+    return SL_OK;
+  };
+  if (!ident && (r = move(T))) return r;
+  const double r2 = max_distance * max_distance;
+  auto evaluate = [&]() -> int {
+    hipLaunchKernelGGL(k_icp_corr, dim3(blocks(n_src)), dim3(kT), 0, s, cur.p, n_src, g, dense.p, ukeys.p, m,
+                       ustart.p, n_tgt, sxyz.p, idx.p, r2, corr.p, d2.p);
+    hipLaunchKernelGGL(k_icp_fold, dim3(blocks(nb)), dim3(kT), 0, s, cur.p, n_src, target, target_normals, corr.p,
+                       d2.p, part.p);
+    MTRY(c, hipGetLastError());
+    MTRY(c, hipMemcpyAsync(hpart.data(), part.p, sizeof(double) * hpart.size(), hipMemcpyDeviceToHost, s));
+    MTRY(c, hipStreamSynchronize(s));
+    for (int k = 0; k < kIcpSums; ++k) sums[k] = 0.0;
+    for (int64_t b = 0; b < nb; ++b)
+      for (int k = 0; k < kIcpSums; ++k) sums[k] = sums[k] + hpart[static_cast<size_t>(kIcpSums * b + k)];
+    const double cnt = sums[28];
+    fit = cnt / static_cast<double>(n_src);
+    rmse = cnt > 0.0 ? std::sqrt(sums[27] / cnt) : 0.0;
+    return SL_OK;
+  };
+  if ((r = evaluate())) return r;
+  for (int it = 0; it < max_iteration; ++it) {
+    double U[16];
+    icp_update(sums, U);  // identity where the system is singular
+    icp_mat4(U, T, T);
+    if ((r = move(U))) return r;
+    const double f0 = fit, r0 = rmse;
+    if ((r = evaluate())) return r;
+    iters = it + 1;
+    if (std::fabs(f0 - fit) < relative_fitness && std::fabs(r0 - rmse) < relative_rmse) break;
+  }
+  return finish();
 }
 
 // Release the scratch buffers the merge pool keeps for `device` (they are

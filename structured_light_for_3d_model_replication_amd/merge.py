@@ -13,10 +13,15 @@ Then ``estimate_normals(KDTreeSearchParamHybrid(radius=2 voxel, max_nn=30))``
 parity is unpinned; oracle/merge_oracle.py is the restatement the tests check
 against.
 
-The reference aligns the views by FPFH + RANSAC + ICP (:145-157).  That
-registration is out of scope.  ``merge_pro_360_posed`` takes the poses instead:
-the turntable's known poses, or the same ones ``Reconstructor.decode_triangulate``
-applies inside k_cloud.
+Registration.  The reference aligns consecutive views by FPFH + RANSAC
+(a global estimate) refined by point-to-plane ICP (:145-157) and accumulates
+the transforms (:159-167).  ``merge_pro_360`` keeps that flow with the ICP on
+the GPU (``registration_icp``: sl_icp_point_to_plane, Open3D's loop and
+point-to-plane step; parity vs Open3D unpinned, oracle/merge_oracle.py
+restates it) and the RANSAC estimate replaced by a seed: the turntable's
+relative pose between the two views (``seed_poses``), or the identity.
+``merge_pro_360_posed`` skips registration and takes the poses as they are
+(the same ones ``Reconstructor.decode_triangulate`` applies inside k_cloud).
 """
 from __future__ import annotations
 
@@ -137,6 +142,126 @@ def estimate_normals(points, radius: float, max_nn: int = 30, *, device=None) ->
         _lib.check(eng._L.sl_estimate_normals(eng._ctx, _ptr(P), n, float(radius), int(max_nn), out.data_ptr(),
                                               eng._stream(None)), eng._ctx, "sl_estimate_normals")
     return out[:n]
+
+
+def registration_icp(source, target, target_normals, max_correspondence_distance: float, init=None, *,
+                     max_iteration: int = 30, relative_fitness: float = 1e-6, relative_rmse: float = 1e-6,
+                     device=None) -> dict:
+    """o3d.pipelines.registration.registration_icp(source, target,
+    max_correspondence_distance, init, TransformationEstimationPointToPlane(),
+    ICPConvergenceCriteria(relative_fitness, relative_rmse, max_iteration))
+    (processing.py:154-156) on the GPU -> {"transformation": 4x4 numpy,
+    "fitness", "inlier_rmse", "iterations"}.  ``target_normals``: the target's
+    normals (estimate_normals, as merge_pro_360 computes them)."""
+    eng = _engine(device)
+    S = _f64(source, eng.device)
+    T = _f64(target, eng.device)
+    N = _f64(target_normals, eng.device)
+    if N.shape != T.shape:
+        raise ValueError("TransformationEstimationPointToPlane requires pre-computed normal vectors for the "
+                         "target point cloud")
+    M0 = np.ascontiguousarray(np.eye(4) if init is None else np.asarray(init, dtype=np.float64).reshape(4, 4))
+    out = np.zeros(16)
+    fit, rmse, it = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    with eng._lock:
+        _lib.check(eng._L.sl_icp_point_to_plane(eng._ctx, _ptr(S) if len(S) else None, S.shape[0],
+                                                _ptr(T) if len(T) else None, _ptr(N) if len(N) else None,
+                                                T.shape[0], float(max_correspondence_distance), M0.ctypes.data,
+                                                int(max_iteration), float(relative_fitness), float(relative_rmse),
+                                                out.ctypes.data, ctypes.byref(fit), ctypes.byref(rmse),
+                                                ctypes.byref(it), eng._stream(None)),
+                   eng._ctx, "sl_icp_point_to_plane")
+    return {"transformation": out.reshape(4, 4), "fitness": fit.value, "inlier_rmse": rmse.value,
+            "iterations": it.value}
+
+
+def rigid_inverse(M) -> np.ndarray:
+    """[R | t]^-1 = [R^T | -(R^T t)] of a rigid 4x4 pose."""
+    M = np.asarray(M, dtype=np.float64).reshape(4, 4)
+    R, t = M[:3, :3], M[:3, 3]
+    out = np.zeros((4, 4))
+    out[:3, :3] = R.T
+    for i in range(3):
+        out[i, 3] = -((R[0, i] * t[0] + R[1, i] * t[1]) + R[2, i] * t[2])
+    out[3, 3] = 1.0
+    return out
+
+
+def mat4(a, b) -> np.ndarray:
+    """Row-major 4x4 product ((a0 b0 + a1 b1) + a2 b2) + a3 b3 (np.dot of
+    processing.py:162, in a fixed order)."""
+    a = np.asarray(a, dtype=np.float64).reshape(4, 4)
+    b = np.asarray(b, dtype=np.float64).reshape(4, 4)
+    out = np.empty((4, 4))
+    for i in range(4):
+        for j in range(4):
+            out[i, j] = ((a[i, 0] * b[0, j] + a[i, 1] * b[1, j]) + a[i, 2] * b[2, j]) + a[i, 3] * b[3, j]
+    return out
+
+
+def merge_pro_360(input_folder, output_path, voxel_size: float = 0.02, *, seed_poses=None, device=None,
+                  binary: bool = True, order: str = "lexicographic", max_iteration: int = 30,
+                  return_transforms: bool = False):
+    """merge_pro_360 (processing.py:116-182): the clouds of ``input_folder``
+    (``ply_files(order)``; default the reference's lexicographic order)
+    registered in sequence -- scan i onto scan i-1 by point-to-plane ICP
+    between their voxel-downsampled clouds (target normals radius 2 voxel,
+    max_nn 30; max correspondence distance = voxel_size; :145-157), the
+    transforms accumulated T_i = T_{i-1} T_local (:159-167) and scan i moved
+    by T_i -- then merged, voxel-downsampled, outlier-filtered, normals
+    estimated and written in Open3D's layout (as merge_pro_360_posed).
+
+    The reference seeds each ICP with an FPFH + RANSAC global estimate; here
+    the seed is ``inverse(seed_poses[i-1]) @ seed_poses[i]`` (the turntable's
+    relative pose between the two views; poses mapping each view into a
+    common frame, e.g. synth.turntable_pose), or the identity when
+    ``seed_poses`` is None.  Returns (points, colors, normals) on the device
+    (+ the accumulated transforms with ``return_transforms``)."""
+    print(f"[Merge 360] Loading clouds from {input_folder}...")
+    files = ply_files(input_folder, order)
+    if len(files) < 2:
+        raise ValueError("Need at least 2 .ply files to merge.")
+    if seed_poses is not None:
+        seed_poses = np.asarray(seed_poses, dtype=np.float64).reshape(-1, 4, 4)
+        if len(seed_poses) != len(files):
+            raise ValueError(f"{len(files)} clouds but {len(seed_poses)} seed poses")
+    eng = _engine(device)
+    pcds = []
+    for f in files:
+        P, C = ply.read_ply(f)
+        pcds.append((torch.from_numpy(np.ascontiguousarray(P, dtype=np.float64)).to(eng.device),
+                     torch.from_numpy(np.ascontiguousarray(C)).to(eng.device)))
+    print(f"[Merge 360] Loaded {len(pcds)} clouds. Running Sequential Registration (New360 Logic)...")
+    down = {}
+
+    def prep(i):  # preprocess_point_cloud (:79-96) without the FPFH features (no RANSAC)
+        if i not in down:
+            Pd, _ = voxel_down_sample(pcds[i][0], None, voxel_size, device=eng.device)
+            down[i] = (Pd, estimate_normals(Pd, voxel_size * 2, 30, device=eng.device))
+        return down[i]
+    accum = np.eye(4)
+    transforms = [accum.copy()]
+    parts_p, parts_c = [pcds[0][0]], [pcds[0][1]]
+    for i in range(1, len(pcds)):
+        print(f"[Merge 360] Aligning Scan {i} -> Scan {i-1}...")
+        src, _ = prep(i)
+        tgt, tgt_n = prep(i - 1)
+        init = np.eye(4) if seed_poses is None else mat4(rigid_inverse(seed_poses[i - 1]), seed_poses[i])
+        T_local = registration_icp(src, tgt, tgt_n, voxel_size, init, max_iteration=max_iteration,
+                                   device=eng.device)["transformation"]
+        accum = mat4(accum, T_local)
+        transforms.append(accum.copy())
+        parts_p.append(transform(pcds[i][0], accum, device=eng.device))
+        parts_c.append(pcds[i][1])
+        down.pop(i - 1, None)
+    merged_p = torch.cat(parts_p)
+    merged_c = torch.cat(parts_c)
+    print("[Merge 360] Post-processing (Downsample + Outlier removal)...")
+    P, C = postprocess(merged_p, merged_c, voxel_size, device=eng.device)
+    N = estimate_normals(P, voxel_size * 2, 30, device=eng.device)
+    ply.save_ply_open3d(P.cpu().numpy(), C.cpu().numpy(), output_path, normals=N.cpu().numpy(), binary=binary)
+    print(f"[Merge 360] Saved merged cloud to {output_path}")
+    return (P, C, N, transforms) if return_transforms else (P, C, N)
 
 
 def pool_trim(device=None) -> int:

@@ -105,3 +105,46 @@ def test_normals_oracle_degenerate_cases():
     plane = np.stack(np.meshgrid(g, g, [0.0], indexing="ij"), -1).reshape(-1, 3)
     N = mo.estimate_normals(plane, 1.5, 30)
     np.testing.assert_array_equal(np.abs(N), np.tile([0.0, 0.0, 1.0], (len(plane), 1)))
+
+
+def _sheet(n_side=90, seed=0):
+    """A bumpy height field (a surface with structure in every direction)."""
+    rng = np.random.default_rng(seed)
+    u, v = np.meshgrid(np.linspace(-60, 60, n_side), np.linspace(-60, 60, n_side))
+    u = u.ravel() + rng.uniform(-0.3, 0.3, u.size)
+    v = v.ravel() + rng.uniform(-0.3, 0.3, v.size)
+    z = 8 * np.sin(u / 13.0) * np.cos(v / 17.0) + 0.004 * u * v
+    return np.stack([u, v, z], 1)
+
+
+def _motion(deg, t):
+    a = np.radians(deg)
+    R = np.array([[np.cos(a), -np.sin(a), 0.0], [np.sin(a), np.cos(a), 0.0], [0.0, 0.0, 1.0]])
+    b = np.radians(deg / 2)
+    R = R @ np.array([[1.0, 0.0, 0.0], [0.0, np.cos(b), -np.sin(b)], [0.0, np.sin(b), np.cos(b)]])
+    M = np.eye(4)
+    M[:3, :3] = R
+    M[:3, 3] = t
+    return M
+
+
+def test_icp_oracle_recovers_a_rigid_motion():
+    """The point-to-plane ICP restatement (processing.py:154-156) converges to
+    a known small motion from the identity: target = M(source)."""
+    from oracle import merge_oracle as m
+    S = _sheet()
+    M = _motion(1.5, [0.8, -0.5, 0.6])
+    T = m._transform(S, M)
+    N = m.estimate_normals(T, 6.0, 30)
+    r = m.registration_icp_point_to_plane(S, T, N, 5.0, None, max_iteration=60)
+    np.testing.assert_allclose(r["transformation"], M, atol=1e-6)
+    assert r["fitness"] == 1.0 and r["inlier_rmse"] < 1e-6 and 0 < r["iterations"] < 60
+
+
+def test_rigid_inverse_and_mat4():
+    from oracle import merge_oracle as m
+    M = _motion(33.0, [10.0, -20.0, 5.0])
+    I = np.array(m.mat4(m.rigid_inverse(M).tolist(), M.tolist()))
+    np.testing.assert_allclose(I, np.eye(4), atol=1e-12)
+    U = m.icp_update([0.0] * 29)  # singular system: the identity update
+    assert np.array_equal(np.array(U), np.eye(4))
