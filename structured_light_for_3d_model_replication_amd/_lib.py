@@ -97,8 +97,14 @@ def load() -> ctypes.CDLL:
                 raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import "
                                    f"__graft_entry__ as g; g.build()'` (hipcc, gfx950)")
             lib = ctypes.CDLL(LIB_PATH)
+            variant = bool(os.environ.get("SLGPU_LIB"))
             for name, (res, args) in _SIGS.items():
-                fn = getattr(lib, name)
+                try:
+                    fn = getattr(lib, name)
+                except AttributeError:
+                    if variant:  # an older measurement build (SLGPU_LIB): entry points it predates are absent
+                        continue
+                    raise
                 fn.restype = res
                 fn.argtypes = args
             _lib = lib

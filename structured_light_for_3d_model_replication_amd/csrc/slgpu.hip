@@ -176,6 +176,7 @@ struct Params {
   const float* xn32;
   const float* yn32;
   float fast_thr;          // k_count's one-compare sufficient |n.r| test (sl_set_calib)
+  int xy_safe;             // every xn, yn entry is div_safe (sl_set_calib): k_cloud skips the per-point test
   const double* nc_rays;   // Nc table [3][HW] or null
   double o0, o1, o2;       // Oc
   const double* poses;
@@ -1726,7 +1727,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       for (int i = 0; i < kPipe; ++i) {
         const double x = ra[i], y = rb[i];
         nrm[i] = sqrt_nr((x * x + y * y) + 1.0);  // s2 in [1, 2^601] when div_safe(x), div_safe(y)
-        if (!(kDivShare && div_safe(x) && div_safe(y))) slow |= 1u << i;
+        if (!(kDivShare && (p.xy_safe || (div_safe(x) && div_safe(y))))) slow |= 1u << i;
       }
       // the three divisions by nrm share one reciprocal (div_rn: the
       // compiler's own f64 division sequence, bit for bit, where it would
@@ -1942,6 +1943,7 @@ struct sl_ctx {
   double* d_yn = nullptr;
   float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H]
   float fast_thr = 0.0f;   // k_count's sufficient |n.r| threshold (Params::fast_thr)
+  bool xy_safe = false;     // every xn / yn table entry is div_safe (Params::xy_safe)
   double* d_nc = nullptr;
   // scratch
   ViewStats* d_stats = nullptr;
@@ -2560,6 +2562,13 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
     HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_nc), sizeof(double) * 3 * HW));
     HIP_TRY(c, hipMemcpy(c->d_nc, Nc, sizeof(double) * 3 * HW, hipMemcpyHostToDevice));
   }
+  {  // the exact k_cloud's shared-reciprocal forms hold for every pixel's (x, y)
+    auto safe = [](double v) { const double m = fabs(v); return m >= 0x1p-300 && m <= 0x1p300; };
+    bool ok = true;
+    for (int u = 0; u < W && ok; ++u) ok = safe(xn[u]);
+    for (int v = 0; v < H && ok; ++v) ok = safe(yn[v]);
+    c->xy_safe = ok;
+  }
   c->Oc[0] = Oc[0];
   c->Oc[1] = Oc[1];
   c->Oc[2] = Oc[2];
@@ -2612,6 +2621,7 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.xn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp : nullptr;
   p.yn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp + c->W : nullptr;
   p.fast_thr = c->fast_thr;
+  p.xy_safe = c->xy_safe ? 1 : 0;
   p.nc_rays = c->d_nc;
   p.o0 = c->Oc[0];
   p.o1 = c->Oc[1];

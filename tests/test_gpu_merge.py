@@ -279,7 +279,9 @@ def test_icp_turntable_views_vs_oracle(mg):
     got = mg.registration_icp(src, tgt, tn, vs, init)
     want = mo.registration_icp_point_to_plane(src.cpu().numpy(), tgt.cpu().numpy(), tn.cpu().numpy(), vs, init)
     _icp_equal(got, want)
-    assert got["fitness"] > 0.5 and got["iterations"] >= 1
+    # (the rendered scene's back wall does not turn with the table: part of
+    # each view has no counterpart within one voxel)
+    assert got["fitness"] > 0.1 and got["iterations"] >= 1
 
 
 def test_icp_edges(mg):
