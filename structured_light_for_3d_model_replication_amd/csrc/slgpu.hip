@@ -118,6 +118,8 @@ constexpr int M_HIST = 64;     // adaptive mask: k_decode builds the histogram, 
 constexpr int M_FAST32 = 128;  // k_cloud: f32 arithmetic for well-conditioned points (SL_XYZ_F32_FAST)
 constexpr int M_PLANE_RSRC = 512;  // k_decode: a buffer descriptor per plane (a view's planes read span >= 2 GiB)
 constexpr int M_TEX = 2048;    // k_cloud: a BGR texture (else the white plane replicated)
+constexpr int M_VERIFY = 4096; // k_cloud, SL_XYZ_F32: a shorter f64 evaluation whose f32 rounding is proven equal
+                               // to the reference's (else the exact sequence); Oc = 0, pinhole rays, no pose
 constexpr int M_DECIDE = 256;  // k_decode: also the mask and the |n.r| decision (k_count's work; k_stats
                                // histograms): mask map, point nibbles, chunk counts, block sums
 constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
@@ -1703,6 +1705,48 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       pl[i] = p.planes[c];
     }
     double X[kPipe], Y[kPipe], Z[kPipe];
+    uint32_t slow = 0u;
+    if (mode & M_VERIFY) {
+      // SL_XYZ_F32 output is float32(P_ref), P_ref the reference's f64 value.
+      // A shorter f64 evaluation P' (rsq and rcp with one Newton step each,
+      // P' = r' t', no correctly rounded sqrt / divisions) gives the same
+      // float32 whenever no float32 rounding midpoint lies within P''s error
+      // of it.  Error bound (u = 2^-53; measured on gfx950 with
+      // scripts/micro/rsq_rcp_accuracy.hip: rsq + Newton <= 38 u, rcp +
+      // Newton <= 20 u, bounded here by 64 u / 32 u): per coordinate
+      // |P' - P_ref| <= (103 + 73 kappa) u |P| with kappa = sum|n_i r_i| /
+      // |n.r| <= 16, i.e. < 2^-42.7 |P| < 2^10.3 f64 ulps of P'.  A coordinate
+      // whose 29 dropped mantissa bits are within 2^13 ulps of the midpoint
+      // pattern 2^28 (or outside 2^-100 <= |P'| < 2^100, or s2 >= 4, or kappa
+      // > 16) sends its point to the exact sequence below: the stored float32
+      // is the reference's bit for bit either way.
+      auto ambiguous = [](double v) {
+        const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+        const unsigned lo = static_cast<unsigned>(b) & 0x1fffffffu;
+        const unsigned ex = static_cast<unsigned>(b >> 52) & 0x7ffu;
+        return (lo - (0x10000000u - 8192u)) <= 16384u || ex < 1023u - 100u || ex >= 1023u + 100u;
+      };
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
+        const double x = ra[i], y = rb[i];
+        const double s2 = (x * x + y * y) + 1.0;
+        const double y0 = __builtin_amdgcn_rsq(s2);
+        const double hy = (0.5 * s2) * y0;
+        const double inv = __builtin_fma(y0, __builtin_fma(-hy, y0, 0.5), y0);  // 1 / sqrt(s2)
+        const double r0 = x * inv, r1 = y * inv;
+        const double a0 = pl[i].x * r0, a1 = pl[i].y * r1, a2 = pl[i].z * inv;
+        const double den = (a0 + a1) + a2;
+        const double S = (fabs(a0) + fabs(a1)) + fabs(a2);
+        const double rc0 = __builtin_amdgcn_rcp(den);
+        const double rc = __builtin_fma(rc0, __builtin_fma(-den, rc0, 1.0), rc0);
+        const double t = -pl[i].w * rc;
+        X[i] = r0 * t;
+        Y[i] = r1 * t;
+        Z[i] = inv * t;
+        const bool ok = s2 < 4.0 && S <= 16.0 * fabs(den) && !ambiguous(X[i]) && !ambiguous(Y[i]) && !ambiguous(Z[i]);
+        if (!ok) slow |= 1u << i;
+      }
+    }
     // The kPipe points' chains (sqrt, shared reciprocal, divisions) carry no
     // branch, so the compiler interleaves them: a point whose operands leave
     // the range where the shortened sequences are bit-identical to the
@@ -1710,7 +1754,11 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
     // with the operators after the loop (a branch the wave skips when no
     // lane needs it).  With a branch per point the chains ran one after the
     // other, each one's full f64 latency exposed.
-    uint32_t slow = 0u;
+    // (M_VERIFY: only for the points the verified route could not settle --
+    // the wave skips this block when no lane has one)
+    const uint32_t exact = (mode & M_VERIFY) ? slow : ((1u << kPipe) - 1u);
+    slow = 0u;
+    if (exact) {
     // stage by stage over the kPipe points (the source order the scheduler
     // keeps): independent instructions of different points sit side by side
     double r0[kPipe], r1[kPipe], r2[kPipe];
@@ -1751,6 +1799,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
     }
 #pragma unroll
     for (int i = 0; i < kPipe; ++i) {
+      if (!((exact >> i) & 1u)) continue;
       X[i] = p.o0 + r0[i] * t[i];
       Y[i] = p.o1 + r1[i] * t[i];
       Z[i] = p.o2 + r2[i] * t[i];
@@ -1760,6 +1809,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         Z[i] = pl[i].w;
       }
     }
+    slow &= exact;
     if (slow) {  // rare: the operators' own sequences (rescaling, +-0, inf / NaN)
 #pragma unroll
       for (int i = 0; i < kPipe; ++i) {
@@ -1782,6 +1832,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         Z[i] = p.o2 + r2 * t;
       }
     }
+    }  // exact
     if (pose) {
 #pragma unroll
       for (int i = 0; i < kPipe; ++i) {
@@ -1895,7 +1946,7 @@ __device__ __forceinline__ long long block_offset(const Params& p, int64_t b, in
 #define SLGPU_CLOUD_WAVES 5
 #endif
 #ifndef SLGPU_EXACT_PIPE
-#define SLGPU_EXACT_PIPE 4
+#define SLGPU_EXACT_PIPE 2
 #endif
 constexpr int kExactPipe = SLGPU_EXACT_PIPE;  // points per lane per pass of the exact (f64) k_cloud<M_TEX>
 template <int MODE, int VEC, int PIPE = kPipe>
@@ -1944,6 +1995,7 @@ struct sl_ctx {
   float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H]
   float fast_thr = 0.0f;   // k_count's sufficient |n.r| threshold (Params::fast_thr)
   bool xy_safe = false;     // every xn / yn table entry is div_safe (Params::xy_safe)
+  bool verify32 = true;     // SL_XYZ_F32 by the verified shorter route (SLGPU_VERIFY32=0: the exact sequence, A/B)
   double* d_nc = nullptr;
   // scratch
   ViewStats* d_stats = nullptr;
@@ -2149,8 +2201,9 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
 KernelFn pick_cloud(int mode, bool vec, bool small) {
   if (vec && small && kSmallPipe > kPipe && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1, kSmallPipe>;
   if (vec && mode == M_TEX) return k_cloud<M_TEX, 1, kExactPipe>;  // f32 xyz, pinhole rays, BGR texture
+  if (vec && mode == (M_VERIFY | M_TEX)) return k_cloud<M_VERIFY | M_TEX, 1, kExactPipe>;  // ... verified route
   if (vec && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1>;
-  return vec ? k_cloud<-1, 1> : k_cloud<-1, 0>;
+  return vec ? k_cloud<-1, 1, kExactPipe> : k_cloud<-1, 0, kExactPipe>;  // (f64 chains: kExactPipe points per pass)
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -2448,6 +2501,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
   if (const char* d = getenv("SLGPU_PATH")) c->force_3k = atoi(d) == 3;
   if (const char* d = getenv("SLGPU_RECORDS")) c->rec_from_maps = atoi(d) == 0;
   if (const char* d = getenv("SLGPU_REC12")) c->rec12 = atoi(d) != 0;
+  if (const char* d = getenv("SLGPU_VERIFY32")) c->verify32 = atoi(d) != 0;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
@@ -2600,9 +2654,11 @@ static int common_out_checks(sl_ctx* c, int n_views, int H, int W, void* xyz, in
 static int xyz_mode_bits(const sl_ctx* c, int xyz_dtype, const double* poses) {
   const int nc_bit = c->d_nc ? M_NC : 0;
   if (xyz_dtype == SL_XYZ_F64) return M_XYZ64 | nc_bit;
-  const bool fast = xyz_dtype == SL_XYZ_F32_FAST && !c->d_nc && !poses && c->Oc[0] == 0.0 &&
-                    c->Oc[1] == 0.0 && c->Oc[2] == 0.0;
-  return fast ? M_FAST32 : nc_bit;
+  const bool simple = !c->d_nc && !poses && c->Oc[0] == 0.0 && c->Oc[1] == 0.0 && c->Oc[2] == 0.0;
+  if (xyz_dtype == SL_XYZ_F32_FAST && simple) return M_FAST32;
+  // SL_XYZ_F32 (and F32_FAST where its bound does not apply): the verified
+  // shorter f64 route where P = r t (Oc = 0, pinhole rays, no pose)
+  return simple && c->verify32 ? M_VERIFY : nc_bit;
 }
 
 static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
