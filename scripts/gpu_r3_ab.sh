@@ -1,7 +1,7 @@
 # Round 3 same-box A/B of library builds on the exact (f64) path: per build,
 # the parity subset (tests/test_gpu_parity.py), then kbench (exact, C2 shape,
 # 300 ms pre-roll, HIP events + back-to-back re-runs) twice interleaved, then
-# one bench.py c2 line.  Arguments: "label|lib" pairs ("default" = in-tree).
+# one bench.py c2 line.  Arguments: "label|lib[|ENV=V ...]" ("default" = in-tree).
 # -> gpurun_out/r3ab
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -11,25 +11,25 @@ mkdir -p $O
 : > $O/kb.log
 : > $O/bench.log
 for spec in "$@"; do
-  IFS='|' read -r label lib <<< "$spec"
+  IFS='|' read -r label lib envs <<< "$spec"
   [ "$lib" = default ] && lib=structured_light_for_3d_model_replication_amd/libslgpu.so
-  SLGPU_LIB=$(realpath $lib) timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "golden_fused or golden_cloud or synthetic or full_4k or multiview" > $O/pytest_$label.log 2>&1 || { echo "parity FAILED for $label"; tail -30 $O/pytest_$label.log; exit 1; }
+  env ${envs:-} SLGPU_LIB=$(realpath $lib) timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "golden_fused or golden_cloud or synthetic or full_4k or multiview" > $O/pytest_$label.log 2>&1 || { echo "parity FAILED for $label"; tail -30 $O/pytest_$label.log; exit 1; }
   echo "$label parity: $(tail -1 $O/pytest_$label.log)"
 done
 for rep in 1 2; do
   for spec in "$@"; do
-    IFS='|' read -r label lib <<< "$spec"
+    IFS='|' read -r label lib envs <<< "$spec"
     [ "$lib" = default ] && lib=structured_light_for_3d_model_replication_amd/libslgpu.so
     for only in ${AB_MODES:-"maps+cloud" "cloud"}; do
-      SLGPU_LIB=$(realpath $lib) timeout -k 10 120 python -u scripts/kbench.py --reps 30 --preroll-ms 300 --only "$only" ${AB_KB:-} 2>&1 | grep variant | grep -v torch_copy | sed "s/^{/{\"label\": \"$label\", /" >> $O/kb.log || exit 1
+      env ${envs:-} SLGPU_LIB=$(realpath $lib) timeout -k 10 120 python -u scripts/kbench.py --reps 30 --preroll-ms 300 --only "$only" ${AB_KB:-} 2>&1 | grep variant | grep -v torch_copy | sed "s/^{/{\"label\": \"$label\", /" >> $O/kb.log || exit 1
     done
   done
 done
 for spec in "$@"; do
-  IFS='|' read -r label lib <<< "$spec"
+  IFS='|' read -r label lib envs <<< "$spec"
   [ "$lib" = default ] && lib=structured_light_for_3d_model_replication_amd/libslgpu.so
   for cfg in ${AB_CONFIGS:-c2}; do
-    SLGPU_LIB=$(realpath $lib) timeout -k 10 300 python -u bench.py --config $cfg --no-cpu-baseline --no-secondary ${AB_BENCH:-} > $O/bench_${label}_$cfg.json 2> $O/bench_${label}_$cfg.err || { tail -20 $O/bench_${label}_$cfg.err; exit 1; }
+    env ${envs:-} SLGPU_LIB=$(realpath $lib) timeout -k 10 300 python -u bench.py --config $cfg --no-cpu-baseline --no-secondary ${AB_BENCH:-} > $O/bench_${label}_$cfg.json 2> $O/bench_${label}_$cfg.err || { tail -20 $O/bench_${label}_$cfg.err; exit 1; }
     python3 -c "
 import json,sys
 d=json.loads(open('$O/bench_${label}_$cfg.json').read().strip().splitlines()[-1])

@@ -676,7 +676,7 @@ def test_verified_f32_route_equals_the_exact_sequence(f_scale, monkeypatch):
     K = np.array(cal["cam_K"], dtype=np.float64)
     K[0, 0] = K[1, 1] = f_scale * rig.W
     cal["cam_K"] = K
-    cal.pop("Nc", None)
+    cal["Nc"] = np.zeros((3, 1))  # no per-pixel table: rays from cam_K (sl_system.py:607-621)
     sth, texh = st.cpu().numpy(), tex.cpu().numpy()
     _, _, _, P, C = o.decode_triangulate(list(sth), texh, cal, 1920, 1080)
     outs = []
