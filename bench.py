@@ -112,6 +112,11 @@ def parse(argv=None):
     ap.add_argument("--cpu-procs", type=int, default=None,
                     help="processes of the multi-process CPU leg (default: the core share, multi-view "
                          "configs only; 0: off)")
+    ap.add_argument("--stack-ready", dest="stack_ready", action="store_true", default=False,
+                    help="declare the resident stacks ready on every call (sl_stack_ready: the histogram pass "
+                         "starts on a side stream beside the previous call's k_cloud; measured slower at c2, "
+                         "DESIGN.md 5.2)")
+    ap.add_argument("--no-stack-ready", dest="stack_ready", action="store_false")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r03_traffic_c2.json"),
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
                          "scripts/traffic_from_pmc.py)")
@@ -438,9 +443,14 @@ def main():
     # --xyz fast; SL_XYZ_F32_FAST applies without a pose (include/slgpu.h)
     head_fast = a.xyz == "fast" and poses is None
 
+    # the stacks are resident in HBM (written once, before the warm-up); with
+    # --stack-ready each call declares them ready (sl_stack_ready), so its
+    # histogram pass may start beside the previous call's k_cloud
+    ready = True if a.stack_ready else None
+
     def step(o, maps=maps, fast=head_fast):
         eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
-                               xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o)
+                               xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o, stack_ready=ready)
         return None
 
     # --streams S: core.ReconstructorPool, S contexts (own scratch, own
@@ -463,7 +473,8 @@ def main():
             return cur
         res = pool.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
                                       xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
-                                      wait_inputs=False)  # resident inputs; outputs never read meanwhile
+                                      wait_inputs=False,  # resident inputs; outputs never read meanwhile
+                                      stack_ready=ready)
         return res["stream"]
 
     def run_steps(k):
@@ -644,7 +655,8 @@ def main():
                                    + ("col/row/mask maps + " if maps else "")
                                    + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
                        "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
-                       "parallelism": f"views sharded over {world} GPU(s)", "streams_per_gpu": S},
+                       "parallelism": f"views sharded over {world} GPU(s)", "streams_per_gpu": S,
+                       "stack_ready": bool(a.stack_ready)},
             "timing": {"preroll": pre,
                        "step_us": spread(step_us),
                        "step_us_note": "HIP events at every step boundary, on the step's stream (completion to "

@@ -129,6 +129,19 @@ int sl_decode_triangulate(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_
  * the kernels count nothing. */
 int sl_mask_counts_to(sl_ctx* ctx, int64_t* device_counts);
 
+/* Stack readiness for the NEXT sl_decode_triangulate on this context (that
+ * call only; consumed even when the call fails): the caller promises that the
+ * stack and texture are in place once `event` (a hipEvent_t recorded by the
+ * caller) has completed, or already now when `event` is NULL (stacks resident
+ * in HBM, or written by work the caller has synchronised).  The call's
+ * adaptive-mask histogram pass (sl_system.py:526-528) then runs on the
+ * context's side stream as soon as that holds and the previous call's decode
+ * has read its own histograms -- beside the previous call's triangulation --
+ * instead of behind everything queued on the call's stream.  Results are
+ * unchanged.  (The later launch groups of one large call always do this.)
+ * Not applied while the call's stream is being captured into a graph. */
+int sl_stack_ready(sl_ctx* ctx, void* event);
+
 /* reconstruct_point_cloud on caller-supplied maps (sl_system.py:584-653).
  * col_map device int32 [n_views][H][W]; mask device uint8 [n_views][H][W]
  * (non-zero = valid); tex_bgr device [n_views][H][W][3].  Outputs as above. */

@@ -82,6 +82,11 @@ for name, kw in [("maps+cloud", dict(maps=True, cloud=True)), ("cloud", dict(map
         eng.decode_triangulate(st, texture=tx, out=out, **kw)
     eng.sync()
     wall_us = 1e6 * (time.perf_counter() - t0) / a.reps
+    t0 = time.perf_counter()  # the same with the stack declared ready (k_stats beside the previous k_cloud)
+    for _ in range(a.reps):
+        eng.decode_triangulate(st, texture=tx, out=out, stack_ready=True, **kw)
+    eng.sync()
+    wall_ready_us = 1e6 * (time.perf_counter() - t0) / a.reps
     npts = int(out["view_offsets"][-1].item()) if "view_offsets" in out else 0
     rr = eng.time_kernels(max(a.reps, 10))  # back-to-back re-runs of each kernel (decode, stats/count, cloud)
     planes = st.shape[1] if kw.get("maps") else 2 + 2 * 11
@@ -90,5 +95,5 @@ for name, kw in [("maps+cloud", dict(maps=True, cloud=True)), ("cloud", dict(map
     print(json.dumps({"variant": name, "count_us": 1e3 * s_ms / n,
                       "decode_us": 1e3 * d_ms / n, "cloud_us": 1e3 * c_ms / n, "total_us": 1e3 * tot,
                       "alg_GBps_total": b / tot / 1e6, "points": npts, "host_us_per_call": host_us,
-                      "wall_us_per_call": wall_us,
+                      "wall_us_per_call": wall_us, "wall_ready_us_per_call": wall_ready_us,
                       "rerun_us": {"decode": 1e3 * rr[0], "stats_count": 1e3 * rr[1], "cloud": 1e3 * rr[2]}, "lib": os.path.basename(os.environ.get("SLGPU_LIB", "libslgpu.so"))}))

@@ -161,7 +161,8 @@ class Reconstructor:
                            texture: torch.Tensor | None = None, mask_mode: str = "adaptive",
                            maps: bool = False, cloud: bool = True, xyz_dtype=torch.float32,
                            poses: torch.Tensor | None = None, fast_f32: bool = False, stream=None,
-                           out: dict | None = None, mask_counts: torch.Tensor | None = None):
+                           out: dict | None = None, mask_counts: torch.Tensor | None = None,
+                           stack_ready=None):
         """Fused decode (+ triangulation) of a device stack.
 
         ``stack`` uint8 [n_img, H, W] or [V, n_img, H, W] on this device;
@@ -176,6 +177,12 @@ class Reconstructor:
         view's number of pixels that pass the mask -- the N of
         reconstruct_point_cloud's "Processing N valid pixels..." line
         (sl_system.py:601-602) -- asynchronously, like the other outputs.
+        ``stack_ready`` (``True`` or a ``torch.cuda.Event``): the caller's
+        promise that the stack and texture are in place now (resident in HBM)
+        or once that event has completed, whatever is queued on ``stream``;
+        the adaptive mask's histogram pass then starts on the context's side
+        stream beside the previous call's triangulation (sl_stack_ready).
+        Results are unchanged.
         """
         if stack.dtype != torch.uint8 or stack.device != self.device:
             raise ValueError("stack must be a uint8 tensor on the reconstructor's device")
@@ -227,6 +234,9 @@ class Reconstructor:
             if mask_counts is not None:
                 _lib.check(self._L.sl_mask_counts_to(self._ctx, mask_counts.data_ptr()), self._ctx,
                            "sl_mask_counts_to")
+            if stack_ready is not None and stack_ready is not False:
+                ev = None if stack_ready is True else ctypes.c_void_p(stack_ready.cuda_event)
+                _lib.check(self._L.sl_stack_ready(self._ctx, ev), self._ctx, "sl_stack_ready")
             _lib.check(self._L.sl_decode_triangulate(
                 self._ctx, stack.data_ptr(), stack.stride(0), V, n_img, H, W, int(n_cols), int(n_rows),
                 _ptr(texture), 3 * H * W if texture is None else texture.stride(0), MASK_MODES[mask_mode],
@@ -456,6 +466,8 @@ class ReconstructorPool:
         caller knows are ready and kept alive (e.g. resident stacks)."""
         if "stream" in kw:
             raise ValueError("ReconstructorPool picks the stream (one per lane)")
+        if not wait_inputs:
+            kw.setdefault("stack_ready", True)  # the caller's promise covers the histogram pass too
         with self._lock:
             i = self._next
             self._next = (i + 1) % len(self.engines)

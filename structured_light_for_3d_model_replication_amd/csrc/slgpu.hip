@@ -2039,6 +2039,20 @@ struct sl_ctx {
   bool done_valid = false;
   int64_t last_launches = 0, last_launch_px = 0;  // sl_last_launch_info
   int64_t* mc_next = nullptr;  // sl_mask_counts_to: the next sl_decode_triangulate's masked-pixel counts
+  // The adaptive mask's histogram pass (k_stats) ahead of its k_decode on a
+  // side stream, beside the previous launch group's k_cloud: for the later
+  // launch groups of a call, and for a call's first group when the caller
+  // declared the stack ready (sl_stack_ready).  Its only scratch is the
+  // parity-buffered histograms, so it waits for no more than the last kernel
+  // that read them (hist_ev) and the caller's readiness event.
+  hipStream_t side = nullptr;
+  hipEvent_t hist_ev = nullptr;   // after the latest kernel that reads the histograms (k_decode / k_count)
+  hipEvent_t stats_ev = nullptr;  // after a k_stats on `side` (its k_decode waits for it)
+  hipEvent_t entry_ev = nullptr;  // the side path's first use: everything queued before it
+  bool hist_tracked = false;      // hist_ev is recorded after every histogram reader from now on
+  bool ready_next = false;        // sl_stack_ready: armed for the next sl_decode_triangulate
+  hipEvent_t ready_ev_next = nullptr;
+  bool no_side = false;           // SLGPU_STATS_SIDE=0: k_stats always on the call's stream (A/B)
   struct {
     bool valid = false;
     bool decide = false;  // fn[1] = k_stats (or null) instead of k_count
@@ -2214,12 +2228,37 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // decode_mode / count_mode / cloud_mode (< 0: no cloud) are the kernels' mode
 // bits.  Launch groups hold at most kMaxChunks chunks (at least one view); a
 // group's points follow the earlier groups' (base_in).
+// The side stream and its events (created on first use).
+int ensure_side(sl_ctx* c) {
+  if (c->side) return SL_OK;
+  for (hipEvent_t* e : {&c->hist_ev, &c->stats_ev, &c->entry_ev})
+    if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+  return SL_OK;
+}
+
+// ready: the caller declared the stack ready (sl_stack_ready; ready_ev, if
+// non-null, completes when it is): the first launch group's k_stats may run on
+// the side stream too.
 int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mode, int cloud_mode,
-           hipStream_t s) {
+           hipStream_t s, bool ready = false, hipEvent_t ready_ev = nullptr) {
   const bool decide = (decode_mode & M_DECIDE) != 0;
   const int64_t cpv = p0.cpv;
   const int vpg = static_cast<int>(std::max<int64_t>(1, kMaxChunks / cpv));  // views per group
+  const int n_groups = static_cast<int>((p0.n_views + vpg - 1) / vpg);
   const bool adaptive = (decode_mode & M_HIST) != 0;
+  // k_stats on the side stream (never while `s` is being captured into a
+  // graph: the side path waits on events recorded outside the capture)
+  bool side_ok = false;
+  if (decide && adaptive && c->prof_ev.empty() && (ready || n_groups > 1) && !c->no_side) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_TRY(c, hipStreamIsCapturing(s, &cs));
+    side_ok = cs == hipStreamCaptureStatusNone;
+    if (side_ok) {
+      int r = ensure_side(c);
+      if (r) return r;
+    }
+  }
   int r = ensure_scratch(c, std::min(vpg, p0.n_views), p0.HW, (decode_mode & M_CODES) != 0);
   if (r) return r;
   r = grow(c, &c->d_stats, &c->cap_stats, p0.n_views);
@@ -2258,11 +2297,28 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     p.ptnib = c->d_ptnib;
     p.chunk_counts = c->d_chunk_counts;
     p.block_sums = c->d_block_sums;
+    // this group's k_stats on the side stream: after the last reader of the
+    // histograms it zeroes (the previous group's or call's k_decode) and, for
+    // a call's first group, the caller's readiness event (else after
+    // everything queued so far: the side path's first use)
+    const bool ahead = side_ok && (g > 0 || ready);
+    hipStream_t ss = ahead ? c->side : s;
+    if (g == 0 && ready_ev && !ahead) HIP_TRY(c, hipStreamWaitEvent(s, ready_ev, 0));  // the promise, kept on s
+    if (ahead) {
+      if (g == 0 && ready_ev) HIP_TRY(c, hipStreamWaitEvent(ss, ready_ev, 0));
+      if (!c->hist_tracked) {
+        HIP_TRY(c, hipEventRecord(c->entry_ev, s));
+        HIP_TRY(c, hipStreamWaitEvent(ss, c->entry_ev, 0));
+        c->hist_tracked = true;
+      } else {
+        HIP_TRY(c, hipStreamWaitEvent(ss, c->hist_ev, 0));
+      }
+    }
     if (adaptive) {  // hist_dirty: leading words of a buffer that may be non-zero
       const int a = c->par, b = 1 - c->par;
       const int64_t words = static_cast<int64_t>(nv) * (decide ? kHistView : kSlot);
       if (c->hist_dirty[a] > 0)
-        HIP_TRY(c, hipMemsetAsync(c->d_hist[a], 0, sizeof(unsigned) * c->hist_dirty[a], s));
+        HIP_TRY(c, hipMemsetAsync(c->d_hist[a], 0, sizeof(unsigned) * c->hist_dirty[a], ss));
       p.hist = c->d_hist[a];
       p.hist_zero = c->d_hist[b];
       c->hist_dirty[a] = words;  // accumulated now; this launch zeroes b's leading `words`
@@ -2302,7 +2358,11 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
         c->last.p[1] = p;
         c->last.fn[1] = reinterpret_cast<const void*>(k_stats);
         c->last.grid[1] = sg;
-        HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(k_stats), sg, dim3(kThreads), args, 0, s));
+        HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(k_stats), sg, dim3(kThreads), args, 0, ss));
+        if (ahead) {
+          HIP_TRY(c, hipEventRecord(c->stats_ev, ss));
+          HIP_TRY(c, hipStreamWaitEvent(s, c->stats_ev, 0));
+        }
       }
       if (gev) HIP_TRY(c, hipEventRecord(gev[1], s));
     }
@@ -2315,6 +2375,10 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->last.fn[0] = reinterpret_cast<const void*>(fn);
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dgrid, dim3(kThreads), args, 0, s));
     }
+    if (adaptive && decide && (c->hist_tracked || (side_ok && g + 1 < n_groups))) {
+      HIP_TRY(c, hipEventRecord(c->hist_ev, s));  // the last reader of this group's histograms
+      c->hist_tracked = true;
+    }
     if (gev) HIP_TRY(c, hipEventRecord(gev[decide ? 2 : 1], s));
     if (!decide) {
       p.mode = count_mode;
@@ -2324,6 +2388,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->last.p[1].masked = nullptr;
       c->last.fn[1] = fn;
       HIP_TRY(c, hipLaunchKernel(fn, grid, dim3(kThreads), args, 0, s));
+      if (adaptive && c->hist_tracked) HIP_TRY(c, hipEventRecord(c->hist_ev, s));  // k_count reads them too
     }
     if (gev && !decide) HIP_TRY(c, hipEventRecord(gev[2], s));
     if (cloud_mode >= 0) {
@@ -2502,6 +2567,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
   if (const char* d = getenv("SLGPU_RECORDS")) c->rec_from_maps = atoi(d) == 0;
   if (const char* d = getenv("SLGPU_REC12")) c->rec12 = atoi(d) != 0;
   if (const char* d = getenv("SLGPU_VERIFY32")) c->verify32 = atoi(d) != 0;
+  if (const char* d = getenv("SLGPU_STATS_SIDE")) c->no_side = atoi(d) == 0;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
@@ -2518,6 +2584,12 @@ void sl_ctx_destroy(sl_ctx* c) {
   }
   if (c->d_gcounts) (void)hipFree(c->d_gcounts);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+  }
+  for (hipEvent_t e : {c->hist_ev, c->stats_ev, c->entry_ev})
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (void* ptr : {static_cast<void*>(c->d_planes), static_cast<void*>(c->d_xn), static_cast<void*>(c->d_yn),
                     static_cast<void*>(c->d_nc), static_cast<void*>(c->d_stats), static_cast<void*>(c->d_f32),
@@ -2692,6 +2764,10 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   if (!c) return SL_EINVAL;
   int64_t* masked = c->mc_next;  // armed by sl_mask_counts_to for this call only (consumed even on failure)
   c->mc_next = nullptr;
+  const bool ready = c->ready_next;  // armed by sl_stack_ready for this call only (likewise)
+  const hipEvent_t ready_ev = c->ready_ev_next;
+  c->ready_next = false;
+  c->ready_ev_next = nullptr;
   int r = common_out_checks(c, n_views, H, W, xyz, xyz_dtype, bgr, cap, view_offsets);
   if (r) return r;
   if (!stack) return fail(c, SL_EINVAL, "stack is NULL");
@@ -2756,7 +2832,15 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   const hipStream_t s = static_cast<hipStream_t>(stream);
   r = stream_handoff(c, s);
   if (r) return r;
-  return launch(c, p, vec, decide ? (decode_mode | M_DECIDE) : decode_mode, count_mode, cloud_mode, s);
+  return launch(c, p, vec, decide ? (decode_mode | M_DECIDE) : decode_mode, count_mode, cloud_mode, s, ready,
+                ready_ev);
+}
+
+int sl_stack_ready(sl_ctx* c, void* event) {
+  if (!c) return SL_EINVAL;
+  c->ready_next = true;
+  c->ready_ev_next = static_cast<hipEvent_t>(event);
+  return SL_OK;
 }
 
 int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, const uint8_t* tex,

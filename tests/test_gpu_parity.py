@@ -693,3 +693,60 @@ def test_verified_f32_route_equals_the_exact_sequence(f_scale, monkeypatch):
         finally:
             e.close()
     np.testing.assert_array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+def _snap(res):
+    """Host copies of a call's maps and cloud (after a sync)."""
+    xyz, bgr, off = _cloud_np(res["cloud"])
+    return (res["col_map"].cpu().numpy(), res["row_map"].cpu().numpy(), res["mask"].cpu().numpy(), xyz, bgr, off)
+
+
+def test_stack_ready_calls_bit_identical():
+    """sl_stack_ready: back-to-back calls over different views on one context,
+    each declaring its stack ready (resident, or ready once an event recorded
+    after a copy on another stream completes), so each call's histogram pass
+    runs on the side stream beside the previous call's k_cloud -- interleaved
+    with a plain call and a fixed-mask call, nothing synchronised in between:
+    every call's maps, mask thresholds and cloud bit-identical to the same call
+    made alone, and view 0's to the oracle."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 480, 640
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    views = [synth.render_stack(rig, seed=900 + v, view_deg=25.0 * v, device="cuda") for v in range(5)]
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    modes = ["adaptive", "adaptive", "fixed", "adaptive", "adaptive"]
+    ref = []
+    for (st, tx), mm in zip(views, modes):
+        ref.append(_snap(eng.decode_triangulate(st, texture=tx, mask_mode=mm, maps=True, cloud=True,
+                                                xyz_dtype=torch.float32, out={})))
+        eng.sync()
+    side = torch.cuda.Stream()
+    for rep in range(2):
+        outs, res, keep = [{} for _ in views], [], []
+        for i, ((st, tx), mm) in enumerate(zip(views, modes)):
+            ready = True if i != 2 or rep == 1 else None
+            if i == 3:  # the stack arrives by a copy on another stream; the event marks it ready
+                buf = torch.empty_like(st)
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    buf.copy_(st)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                # (the call's stream does not wait for the copy: its k_decode waits
+                # for the side stream's k_stats, which waits for the event)
+                keep.append(buf)
+                st, ready = buf, ev
+            res.append(eng.decode_triangulate(st, texture=tx, mask_mode=mm, maps=True, cloud=True,
+                                              xyz_dtype=torch.float32, out=outs[i], stack_ready=ready))
+        eng.sync()
+        for i, r in enumerate(res):
+            got = _snap(r)
+            for a, b in zip(got, ref[i]):
+                np.testing.assert_array_equal(a, b, err_msg=f"call {i}, rep {rep}")
+    st, tx = views[0]
+    col, row, mask, P, C = o.decode_triangulate(list(st.cpu().numpy()), tx.cpu().numpy(), cal)
+    np.testing.assert_array_equal(ref[0][0][0], col)
+    np.testing.assert_array_equal(ref[0][2][0], mask)
+    _assert_f32(ref[0][3], P)
