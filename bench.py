@@ -668,7 +668,9 @@ def main():
                          "achieved": path_gbps, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": path_gbps / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": (f"PMC, {os.path.relpath(a.traffic, REPO)} (committed rocprofv3 "
-                                            "FETCH_SIZE x 2 + WRITE_SIZE of this command, per step)")
+                                            "FETCH_SIZE / WRITE_SIZE passes of this step's kernels, per step, "
+                                            "each counter calibrated on known byte counts of the kernels' "
+                                            "access widths: scripts/micro/store_calib)")
                                            if traffic is not None else None,
                          "algorithmic_bytes_per_step": path_b,
                          "bytes_note": f"SURVEY.md 8(d): {read_planes} stack planes read + 3 B/px BGR texture + "

@@ -47,6 +47,21 @@ __global__ __launch_bounds__(256) void pts(F3* xyz, uint8_t* bgr, int64_t n) {
   }
 }
 
+// FETCH_SIZE of k_cloud's read widths: 8 B per lane (its 12-bit records, 24 B
+// per lane as three 8-B loads) and 16 B per lane (the texture), streaming
+__global__ __launch_bounds__(256) void ld8(const unsigned long long* in, int64_t n, unsigned long long* sink) {
+  unsigned long long acc = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256)
+    acc ^= in[i];
+  if (acc == 0x123456789ull) sink[0] = acc;
+}
+__global__ __launch_bounds__(256) void ld16(const v4u* in, int64_t n, v4u* sink) {
+  v4u acc = {0, 0, 0, 0};
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256)
+    acc ^= in[i];
+  if (acc.x == 0x1234567u) sink[0] = acc;
+}
+
 int main() {
   void *a, *b;
   if (hipMalloc(&a, 16 * kPts + 256) != hipSuccess || hipMalloc(&b, 3 * kPts + 256) != hipSuccess) return 1;
@@ -58,10 +73,15 @@ int main() {
     hipLaunchKernelGGL(st12, g, t, 0, 0, static_cast<F3*>(a), kPts);   // 12 * kPts
     hipLaunchKernelGGL(st3, g, t, 0, 0, static_cast<uint8_t*>(b), kPts);  // 3 * kPts
     hipLaunchKernelGGL(pts, g, t, 0, 0, static_cast<F3*>(a), static_cast<uint8_t*>(b), kPts);  // 15 * kPts
+    hipLaunchKernelGGL(ld8, g, t, 0, 0, static_cast<const unsigned long long*>(a), 2 * kPts,
+                       static_cast<unsigned long long*>(b));  // reads 16 * kPts
+    hipLaunchKernelGGL(ld16, g, t, 0, 0, static_cast<const v4u*>(a), kPts, static_cast<v4u*>(b));  // 16 * kPts
   }
   if (hipDeviceSynchronize() != hipSuccess) return 2;
-  printf("{\"points\": %lld, \"bytes\": {\"st16\": %lld, \"st12\": %lld, \"st3\": %lld, \"pts\": %lld}}\n",
+  printf("{\"points\": %lld, \"bytes\": {\"st16\": %lld, \"st12\": %lld, \"st3\": %lld, \"pts\": %lld, "
+         "\"ld8\": %lld, \"ld16\": %lld}}\n",
          static_cast<long long>(kPts), static_cast<long long>(16 * kPts), static_cast<long long>(12 * kPts),
-         static_cast<long long>(3 * kPts), static_cast<long long>(15 * kPts));
+         static_cast<long long>(3 * kPts), static_cast<long long>(15 * kPts), static_cast<long long>(16 * kPts),
+         static_cast<long long>(16 * kPts));
   return 0;
 }

@@ -119,7 +119,8 @@ constexpr int M_FAST32 = 128;  // k_cloud: f32 arithmetic for well-conditioned p
 constexpr int M_PLANE_RSRC = 512;  // k_decode: a buffer descriptor per plane (a view's planes read span >= 2 GiB)
 constexpr int M_TEX = 2048;    // k_cloud: a BGR texture (else the white plane replicated)
 constexpr int M_VERIFY = 4096; // k_cloud, SL_XYZ_F32: a shorter f64 evaluation whose f32 rounding is proven equal
-                               // to the reference's (else the exact sequence); Oc = 0, pinhole rays, no pose
+                               // to the reference's (else the operators' sequences); Oc = 0, pinhole rays
+                               // (with or without a pose)
 constexpr int M_DECIDE = 256;  // k_decode: also the mask and the |n.r| decision (k_count's work; k_stats
                                // histograms): mask map, point nibbles, chunk counts, block sums
 constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
@@ -135,11 +136,17 @@ constexpr int kHistStride = kHistRep + 1;  // bin stride: replica r of bin b sit
 // point math, 2 = k_cloud without xyz/colour stores, 4 = k_cloud without
 // operand gathers, 8 = k_cloud stops after its loads + rank scan, 16 = ... after
 // the LDS compaction, 32 = k_count with the fixed thresholds, 64 = k_count
-// without the |n.r| test, 128 = k_count without plane gathers.
+// without the |n.r| test, 128 = k_count without plane gathers, 1024 = exact k_cloud gathers
+// its planes from a 32-entry table (cache footprint), 4096 = exact k_cloud without any point
+// arithmetic.
 #ifndef SLGPU_ABLATE
 #define SLGPU_ABLATE 0
 #endif
 constexpr int kAblate = SLGPU_ABLATE;
+#ifndef SLGPU_XY_CALC
+#define SLGPU_XY_CALC 1
+#endif
+constexpr bool kXyCalc = SLGPU_XY_CALC != 0;  // exact k_cloud: rays' x / y by xy_of where sl_set_calib verified it
 constexpr int kMaxWp = 32768;              // projector columns (record codes are 15 bits)
 #ifndef SLGPU_MAX_CHUNKS
 #define SLGPU_MAX_CHUNKS (1 << 16)
@@ -179,6 +186,9 @@ struct Params {
   const float* yn32;
   float fast_thr;          // k_count's one-compare sufficient |n.r| test (sl_set_calib)
   int xy_safe;             // every xn, yn entry is div_safe (sl_set_calib): k_cloud skips the per-point test
+  int xy_calc;             // k_cloud computes xn / yn (xy_of) instead of gathering them: sl_set_calib
+                           // checked on the device that xy_of gives every table entry bit for bit
+  double cx, cy, fx, fy;   // cam_K's (sl_system.py:610-611), for xy_of
   const double* nc_rays;   // Nc table [3][HW] or null
   double o0, o1, o2;       // Oc
   const double* poses;
@@ -318,6 +328,14 @@ __device__ __forceinline__ double sqrt_nr(double s) {
   d = __builtin_fma(-g, g, s);
   return __builtin_fma(d, h, g);
 }
+// (w - c) / f of an integer pixel coordinate w (sl_system.py:615-616) by the
+// shortened division (the quotient is correctly rounded where the operands
+// are in range): sl_set_calib compares it with every xn / yn table entry on
+// the device (k_xy_check) before k_cloud may compute the rays' x / y instead
+// of gathering them.
+__device__ __forceinline__ double xy_of(int w, double c, double f) {
+  return div_rn(static_cast<double>(w) - c, f, recip_nr(f));
+}
 __device__ __forceinline__ bool div_safe(double v) {
   const double m = fabs(v);
   return m >= 0x1p-300 && m <= 0x1p300;
@@ -433,6 +451,17 @@ __device__ __forceinline__ bool has_point(const Params& p, int mode, const float
   return has_point_f64(p.planes, p.xn, p.yn, (mode & M_NC) ? p.nc_rays : nullptr, p.HW, c, u, v, q);
 }
 
+
+// sl_set_calib: does xy_of give every xn / yn table entry bit for bit?
+// (*bad = 1 on any difference; one thread per entry)
+__global__ __launch_bounds__(256) void k_xy_check(const double* xn, int W, const double* yn, int H, double cx,
+                                                  double cy, double fx, double fy, int* bad) {
+  const int i = static_cast<int>(blockIdx.x) * 256 + static_cast<int>(threadIdx.x);
+  bool diff = false;
+  if (i < W) diff = __double_as_longlong(xy_of(i, cx, fx)) != __double_as_longlong(xn[i]);
+  else if (i < W + H) diff = __double_as_longlong(xy_of(i - W, cy, fy)) != __double_as_longlong(yn[i - W]);
+  if (diff) *bad = 1;
+}
 
 // ------------------------------------------------------------------ k_stats ----
 // The adaptive mask's two global reductions (sl_system.py:526-528) ahead of a
@@ -1699,52 +1728,96 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       } else {
         int uu, vv;
         chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
-        ra[i] = p.xn[uu];
-        rb[i] = p.yn[vv];
+        if (kXyCalc && p.xy_calc) {  // (uniform) the table values, computed: no 16 B of gathers per point
+          ra[i] = xy_of(uu, p.cx, p.fx);
+          rb[i] = xy_of(vv, p.cy, p.fy);
+        } else {
+          ra[i] = p.xn[uu];
+          rb[i] = p.yn[vv];
+        }
       }
-      pl[i] = p.planes[c];
+      pl[i] = p.planes[(dbg & 1024) ? (c & 31u) : c];  // (1024: measurement only, a 1-KB plane table)
     }
     double X[kPipe], Y[kPipe], Z[kPipe];
     uint32_t slow = 0u;
+    if (dbg & 4096) {  // measurement only: no point arithmetic at all (operands stored as the point)
+#pragma unroll
+      for (int i = 0; i < kPipe; ++i) {
+        X[i] = ra[i];
+        Y[i] = rb[i];
+        Z[i] = pl[i].w + pl[i].x;
+      }
+    } else {
     if (mode & M_VERIFY) {
-      // SL_XYZ_F32 output is float32(P_ref), P_ref the reference's f64 value.
-      // A shorter f64 evaluation P' (rsq and rcp with one Newton step each,
-      // P' = r' t', no correctly rounded sqrt / divisions) gives the same
-      // float32 whenever no float32 rounding midpoint lies within P''s error
-      // of it.  Error bound (u = 2^-53; measured on gfx950 with
-      // scripts/micro/rsq_rcp_accuracy.hip: rsq + Newton <= 38 u, rcp +
-      // Newton <= 20 u, bounded here by 64 u / 32 u): per coordinate
-      // |P' - P_ref| <= (103 + 73 kappa) u |P| with kappa = sum|n_i r_i| /
-      // |n.r| <= 16, i.e. < 2^-42.7 |P| < 2^10.3 f64 ulps of P'.  A coordinate
-      // whose 29 dropped mantissa bits are within 2^13 ulps of the midpoint
-      // pattern 2^28 (or outside 2^-100 <= |P'| < 2^100, or s2 >= 4, or kappa
-      // > 16) sends its point to the exact sequence below: the stored float32
-      // is the reference's bit for bit either way.
-      auto ambiguous = [](double v) {
-        const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
-        const unsigned lo = static_cast<unsigned>(b) & 0x1fffffffu;
-        const unsigned ex = static_cast<unsigned>(b >> 52) & 0x7ffu;
-        return (lo - (0x10000000u - 8192u)) <= 16384u || ex < 1023u - 100u || ex >= 1023u + 100u;
+      // SL_XYZ_F32 output is float32(P_ref), P_ref the reference's f64 value
+      // (sl_system.py:614-648 with Oc = 0, pinhole rays, no pose).  With
+      // v = (x, y, 1) and r = v / |v|, P = r t = v q where q = -w / (n . v):
+      // the ray's norm cancels, so a shorter f64 evaluation P' = v q' (q' by
+      // reciprocal + two Newton steps, no sqrt, no normalisation) gives the
+      // same float32 whenever no float32 rounding midpoint lies between P'
+      // and P_ref.  Error bound (u = 2^-53, kappa = sum|n_i v_i| / |n . v| =
+      // sum|n_i r_i| / |n . r|): the reference's chain (s2: 3u, |v|: 2.5u,
+      // r: 3.5u, den: 6.5u kappa, t: +u, P: +u) is within (5.5 + 6.5 kappa) u
+      // |P| of the exact P, P' within (4 + 3 kappa) u |P|, so |P' - P_ref| <=
+      // (9.5 + 9.5 kappa) u |P| < 2^7.3 u |P| < 2^8 f64 ulps of P for kappa
+      // <= 16.  A coordinate whose 29 dropped mantissa bits lie within 2^13
+      // ulps of the midpoint pattern 2^28, or outside 2^-100 <= |P'| < 2^100
+      // (zeros, signs of zero, inf / NaN), or a point with kappa > 16 or
+      // sum|n_i v_i| or |w| below 2^-500, goes to the operators' sequences below:
+      // the stored float32 is the reference's bit for bit either way
+      // (tests/test_gpu_parity.py compares the two routes).
+      // (bitwise, not short-circuit: the tests stay branch-free VALU / SALU.
+      // The host takes this route only when every table x, y has 2^-20 <=
+      // |x|, |y| <= 2^20 (xy_plain), so 2^-80 <= |Z| < 2^80 puts X, Y and Z
+      // in 2^-100 .. 2^100: normal float32 values, no zeros)
+      auto ambiguous = [](double v) -> bool {
+        const unsigned lo = static_cast<unsigned>(__double_as_longlong(v)) & 0x1fffffffu;
+        return (lo - (0x10000000u - 8192u)) <= 16384u;
+      };
+      auto out_of_range = [](double v) -> bool {
+        const unsigned ex = static_cast<unsigned>(static_cast<unsigned long long>(__double_as_longlong(v)) >> 52) & 0x7ffu;
+        return (ex - (1023u - 80u)) >= 160u;
       };
 #pragma unroll
       for (int i = 0; i < kPipe; ++i) {
         const double x = ra[i], y = rb[i];
-        const double s2 = (x * x + y * y) + 1.0;
-        const double y0 = __builtin_amdgcn_rsq(s2);
-        const double hy = (0.5 * s2) * y0;
-        const double inv = __builtin_fma(y0, __builtin_fma(-hy, y0, 0.5), y0);  // 1 / sqrt(s2)
-        const double r0 = x * inv, r1 = y * inv;
-        const double a0 = pl[i].x * r0, a1 = pl[i].y * r1, a2 = pl[i].z * inv;
-        const double den = (a0 + a1) + a2;
-        const double S = (fabs(a0) + fabs(a1)) + fabs(a2);
-        const double rc0 = __builtin_amdgcn_rcp(den);
-        const double rc = __builtin_fma(rc0, __builtin_fma(-den, rc0, 1.0), rc0);
-        const double t = -pl[i].w * rc;
-        X[i] = r0 * t;
-        Y[i] = r1 * t;
-        Z[i] = inv * t;
-        const bool ok = s2 < 4.0 && S <= 16.0 * fabs(den) && !ambiguous(X[i]) && !ambiguous(Y[i]) && !ambiguous(Z[i]);
-        if (!ok) slow |= 1u << i;
+        const double b0 = pl[i].x * x, b1 = pl[i].y * y;
+        const double dv = (b0 + b1) + pl[i].z;                    // n . v
+        const double S = (fabs(b0) + fabs(b1)) + fabs(pl[i].z);  // sum |n_i v_i|
+        const double q = -pl[i].w * recip_nr(dv);
+        X[i] = x * q;
+        Y[i] = y * q;
+        Z[i] = q;
+        bool bad = (S > 16.0 * fabs(dv)) | !(S >= 0x1p-500) | !(fabs(pl[i].w) >= 0x1p-500) | out_of_range(Z[i]);
+        if (pose) {
+          // the turntable pose (the epilogue's order, below) on P': each output
+          // k is within (161.5 + 8) u M_k of the epilogue on P_ref, M_k =
+          // sum_j |m_kj P_j| + |m_k3| (P' within 161.5 u |P_j| per coordinate,
+          // the two evaluations' roundings 4 u M_k each) < 2^-45.6 M_k; the
+          // point is settled when float32(v - B) == float32(v + B), B =
+          // 2^-44 M_k, a normal float32 (then the reference's value, inside
+          // that interval, has the same float32)
+          auto unsettled = [](double v, double m) -> bool {
+            const double B = m * 0x1p-44;
+            const uint32_t a = __float_as_uint(static_cast<float>(v - B));
+            const uint32_t b = __float_as_uint(static_cast<float>(v + B));
+            return (a != b) | (((a >> 23) & 0xffu) - 1u >= 254u);
+          };
+          const double x0 = X[i], x1 = Y[i], x2 = Z[i];
+          const double X2 = ((pm[0] * x0 + pm[1] * x1) + pm[2] * x2) + pm[3];
+          const double Y2 = ((pm[4] * x0 + pm[5] * x1) + pm[6] * x2) + pm[7];
+          const double Z2 = ((pm[8] * x0 + pm[9] * x1) + pm[10] * x2) + pm[11];
+          const double M0 = ((fabs(pm[0] * x0) + fabs(pm[1] * x1)) + fabs(pm[2] * x2)) + fabs(pm[3]);
+          const double M1 = ((fabs(pm[4] * x0) + fabs(pm[5] * x1)) + fabs(pm[6] * x2)) + fabs(pm[7]);
+          const double M2 = ((fabs(pm[8] * x0) + fabs(pm[9] * x1)) + fabs(pm[10] * x2)) + fabs(pm[11]);
+          bad |= unsettled(X2, M0) | unsettled(Y2, M1) | unsettled(Z2, M2);
+          X[i] = X2;
+          Y[i] = Y2;
+          Z[i] = Z2;
+        } else {
+          bad |= ambiguous(X[i]) | ambiguous(Y[i]) | ambiguous(Z[i]);
+        }
+        slow |= static_cast<uint32_t>(bad) << i;
       }
     }
     // The kPipe points' chains (sqrt, shared reciprocal, divisions) carry no
@@ -1754,11 +1827,12 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
     // with the operators after the loop (a branch the wave skips when no
     // lane needs it).  With a branch per point the chains ran one after the
     // other, each one's full f64 latency exposed.
-    // (M_VERIFY: only for the points the verified route could not settle --
-    // the wave skips this block when no lane has one)
-    const uint32_t exact = (mode & M_VERIFY) ? slow : ((1u << kPipe) - 1u);
+    // (M_VERIFY: not compiled -- the points the verified route could not
+    // settle take the operators' sequences below, one by one: a branch the
+    // wave skips when no lane has one, and no registers held for the chains)
+    uint32_t fallback = (mode & M_VERIFY) ? slow : 0u;  // points for the operators' own sequences
     slow = 0u;
-    if (exact) {
+    if (!(mode & M_VERIFY)) {
     // stage by stage over the kPipe points (the source order the scheduler
     // keeps): independent instructions of different points sit side by side
     double r0[kPipe], r1[kPipe], r2[kPipe];
@@ -1799,7 +1873,6 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
     }
 #pragma unroll
     for (int i = 0; i < kPipe; ++i) {
-      if (!((exact >> i) & 1u)) continue;
       X[i] = p.o0 + r0[i] * t[i];
       Y[i] = p.o1 + r1[i] * t[i];
       Z[i] = p.o2 + r2[i] * t[i];
@@ -1809,31 +1882,53 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         Z[i] = pl[i].w;
       }
     }
-    slow &= exact;
-    if (slow) {  // rare: the operators' own sequences (rescaling, +-0, inf / NaN)
+    fallback = slow;
+    }  // !M_VERIFY
+    if (fallback) {  // rare: the operators' own sequences (rescaling, +-0, inf / NaN; unsettled M_VERIFY points)
 #pragma unroll
       for (int i = 0; i < kPipe; ++i) {
-        if (!((slow >> i) & 1u)) continue;
+        if (!((fallback >> i) & 1u)) continue;
+        // the point's operands again (M_VERIFY: re-read, so that nothing of
+        // the verified route stays live across this block)
+        double xa = ra[i], xb = rb[i], xc = rcz[i];
+        double4 pp = pl[i];
+        if ((mode & M_VERIFY) && !(dbg & 4)) {
+          const uint32_t e = s_ent[min(j0 + 64 * i + lane, total - 1)];
+          int uu, vv;
+          chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
+          xa = p.xn[uu];
+          xb = p.yn[vv];
+          pp = p.planes[(dbg & 1024) ? (ent_code(e) & 31u) : ent_code(e)];
+        }
         double r0, r1, r2;
         if (mode & M_NC) {
-          r0 = ra[i];
-          r1 = rb[i];
-          r2 = rcz[i];
+          r0 = xa;
+          r1 = xb;
+          r2 = xc;
         } else {
-          const double x = ra[i], y = rb[i];
+          const double x = xa, y = xb;
           const double nrm = sqrt((x * x + y * y) + 1.0);
           r0 = x / nrm;
           r1 = y / nrm;
           r2 = 1.0 / nrm;
         }
-        const double t = -pl[i].w / ((pl[i].x * r0 + pl[i].y * r1) + pl[i].z * r2);
+        const double4 pq = pp;
+        const double t = -pq.w / ((pq.x * r0 + pq.y * r1) + pq.z * r2);
         X[i] = p.o0 + r0 * t;
         Y[i] = p.o1 + r1 * t;
         Z[i] = p.o2 + r2 * t;
+        if ((mode & M_VERIFY) && pose) {  // (M_VERIFY: its settled points are posed above)
+          const double X2 = ((pm[0] * X[i] + pm[1] * Y[i]) + pm[2] * Z[i]) + pm[3];
+          const double Y2 = ((pm[4] * X[i] + pm[5] * Y[i]) + pm[6] * Z[i]) + pm[7];
+          const double Z2 = ((pm[8] * X[i] + pm[9] * Y[i]) + pm[10] * Z[i]) + pm[11];
+          X[i] = X2;
+          Y[i] = Y2;
+          Z[i] = Z2;
+        }
       }
     }
-    }  // exact
-    if (pose) {
+    }  // dbg & 4096
+    if (pose && !(mode & M_VERIFY)) {
 #pragma unroll
       for (int i = 0; i < kPipe; ++i) {
         const double X2 = ((pm[0] * X[i] + pm[1] * Y[i]) + pm[2] * Z[i]) + pm[3];
@@ -1949,6 +2044,10 @@ __device__ __forceinline__ long long block_offset(const Params& p, int64_t b, in
 #define SLGPU_EXACT_PIPE 2
 #endif
 constexpr int kExactPipe = SLGPU_EXACT_PIPE;  // points per lane per pass of the exact (f64) k_cloud<M_TEX>
+#ifndef SLGPU_VERIFY_PIPE
+#define SLGPU_VERIFY_PIPE 2
+#endif
+constexpr int kVerifyPipe = SLGPU_VERIFY_PIPE;  // ... of the verified-route k_cloud<M_VERIFY | M_TEX>
 template <int MODE, int VEC, int PIPE = kPipe>
 __global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : SLGPU_CLOUD_WAVES) void k_cloud(Params p) {
   __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
@@ -1995,6 +2094,10 @@ struct sl_ctx {
   float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H]
   float fast_thr = 0.0f;   // k_count's sufficient |n.r| threshold (Params::fast_thr)
   bool xy_safe = false;     // every xn / yn table entry is div_safe (Params::xy_safe)
+  bool xy_calc = false;     // xy_of reproduces every xn / yn entry (k_xy_check; SLGPU_XY_CALC=0: gathers, A/B)
+  bool xy_plain = false;    // every xn / yn entry has 2^-20 <= |v| <= 2^20 (the verified route's range premise)
+  bool xy_calc_env = true;
+  double cam[4] = {0, 0, 1, 1};  // cx, cy, fx, fy
   bool verify32 = true;     // SL_XYZ_F32 by the verified shorter route (SLGPU_VERIFY32=0: the exact sequence, A/B)
   double* d_nc = nullptr;
   // scratch
@@ -2053,6 +2156,9 @@ struct sl_ctx {
   bool ready_next = false;        // sl_stack_ready: armed for the next sl_decode_triangulate
   hipEvent_t ready_ev_next = nullptr;
   bool no_side = false;           // SLGPU_STATS_SIDE=0: k_stats always on the call's stream (A/B)
+  bool side_groups = false;       // SLGPU_STATS_SIDE=1: also the later launch groups of every call (A/B;
+                                  // off by default: a cross-stream event wait measured 10-20 us of latency,
+                                  // more than the k_stats it hides)
   struct {
     bool valid = false;
     bool decide = false;  // fn[1] = k_stats (or null) instead of k_count
@@ -2215,7 +2321,7 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
 KernelFn pick_cloud(int mode, bool vec, bool small) {
   if (vec && small && kSmallPipe > kPipe && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1, kSmallPipe>;
   if (vec && mode == M_TEX) return k_cloud<M_TEX, 1, kExactPipe>;  // f32 xyz, pinhole rays, BGR texture
-  if (vec && mode == (M_VERIFY | M_TEX)) return k_cloud<M_VERIFY | M_TEX, 1, kExactPipe>;  // ... verified route
+  if (vec && mode == (M_VERIFY | M_TEX)) return k_cloud<M_VERIFY | M_TEX, 1, kVerifyPipe>;  // ... verified route
   if (vec && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1>;
   return vec ? k_cloud<-1, 1, kExactPipe> : k_cloud<-1, 0, kExactPipe>;  // (f64 chains: kExactPipe points per pass)
 }
@@ -2250,7 +2356,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
   // k_stats on the side stream (never while `s` is being captured into a
   // graph: the side path waits on events recorded outside the capture)
   bool side_ok = false;
-  if (decide && adaptive && c->prof_ev.empty() && (ready || n_groups > 1) && !c->no_side) {
+  if (decide && adaptive && c->prof_ev.empty() && (ready || (n_groups > 1 && c->side_groups)) && !c->no_side) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIP_TRY(c, hipStreamIsCapturing(s, &cs));
     side_ok = cs == hipStreamCaptureStatusNone;
@@ -2301,7 +2407,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     // histograms it zeroes (the previous group's or call's k_decode) and, for
     // a call's first group, the caller's readiness event (else after
     // everything queued so far: the side path's first use)
-    const bool ahead = side_ok && (g > 0 || ready);
+    const bool ahead = side_ok && ((g > 0 && c->side_groups) || (g == 0 && ready));
     hipStream_t ss = ahead ? c->side : s;
     if (g == 0 && ready_ev && !ahead) HIP_TRY(c, hipStreamWaitEvent(s, ready_ev, 0));  // the promise, kept on s
     if (ahead) {
@@ -2375,7 +2481,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->last.fn[0] = reinterpret_cast<const void*>(fn);
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dgrid, dim3(kThreads), args, 0, s));
     }
-    if (adaptive && decide && (c->hist_tracked || (side_ok && g + 1 < n_groups))) {
+    if (adaptive && decide && (c->hist_tracked || (side_ok && c->side_groups && g + 1 < n_groups))) {
       HIP_TRY(c, hipEventRecord(c->hist_ev, s));  // the last reader of this group's histograms
       c->hist_tracked = true;
     }
@@ -2567,7 +2673,11 @@ int sl_ctx_create(int device, sl_ctx** out) {
   if (const char* d = getenv("SLGPU_RECORDS")) c->rec_from_maps = atoi(d) == 0;
   if (const char* d = getenv("SLGPU_REC12")) c->rec12 = atoi(d) != 0;
   if (const char* d = getenv("SLGPU_VERIFY32")) c->verify32 = atoi(d) != 0;
-  if (const char* d = getenv("SLGPU_STATS_SIDE")) c->no_side = atoi(d) == 0;
+  if (const char* d = getenv("SLGPU_STATS_SIDE")) {
+    c->no_side = atoi(d) == 0;
+    c->side_groups = atoi(d) == 1;
+  }
+  if (const char* d = getenv("SLGPU_XY_CALC")) c->xy_calc_env = atoi(d) != 0;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
@@ -2694,6 +2804,31 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
     for (int u = 0; u < W && ok; ++u) ok = safe(xn[u]);
     for (int v = 0; v < H && ok; ++v) ok = safe(yn[v]);
     c->xy_safe = ok;
+    auto plain = [](double v) { const double m = fabs(v); return m >= 0x1p-20 && m <= 0x1p20; };
+    ok = true;
+    for (int u = 0; u < W && ok; ++u) ok = plain(xn[u]);
+    for (int v = 0; v < H && ok; ++v) ok = plain(yn[v]);
+    c->xy_plain = ok;
+  }
+  c->cam[0] = cx;
+  c->cam[1] = cy;
+  c->cam[2] = fx;
+  c->cam[3] = fy;
+  c->xy_calc = false;
+  if (c->xy_calc_env) {  // may k_cloud compute the rays' x / y?  Checked on the device, entry by entry
+    int* d_bad = nullptr;
+    HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&d_bad), sizeof(int)));
+    int bad = 0;
+    hipError_t e = hipMemcpy(d_bad, &bad, sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(k_xy_check, dim3((W + H + 255) / 256), dim3(256), 0, nullptr, c->d_xn, W, c->d_yn, H, cx,
+                         cy, fx, fy, d_bad);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    if (e != hipSuccess) return fail(c, SL_EHIP, hipGetErrorString(e));
+    c->xy_calc = bad == 0;
   }
   c->Oc[0] = Oc[0];
   c->Oc[1] = Oc[1];
@@ -2726,11 +2861,11 @@ static int common_out_checks(sl_ctx* c, int n_views, int H, int W, void* xyz, in
 static int xyz_mode_bits(const sl_ctx* c, int xyz_dtype, const double* poses) {
   const int nc_bit = c->d_nc ? M_NC : 0;
   if (xyz_dtype == SL_XYZ_F64) return M_XYZ64 | nc_bit;
-  const bool simple = !c->d_nc && !poses && c->Oc[0] == 0.0 && c->Oc[1] == 0.0 && c->Oc[2] == 0.0;
-  if (xyz_dtype == SL_XYZ_F32_FAST && simple) return M_FAST32;
+  const bool pinhole0 = !c->d_nc && c->Oc[0] == 0.0 && c->Oc[1] == 0.0 && c->Oc[2] == 0.0;
+  if (xyz_dtype == SL_XYZ_F32_FAST && pinhole0 && !poses) return M_FAST32;
   // SL_XYZ_F32 (and F32_FAST where its bound does not apply): the verified
-  // shorter f64 route where P = r t (Oc = 0, pinhole rays, no pose)
-  return simple && c->verify32 ? M_VERIFY : nc_bit;
+  // shorter f64 route where P = r t (Oc = 0, pinhole rays; with or without a pose)
+  return pinhole0 && c->verify32 && c->xy_plain ? M_VERIFY : nc_bit;
 }
 
 static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
@@ -2750,6 +2885,11 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.yn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp + c->W : nullptr;
   p.fast_thr = c->fast_thr;
   p.xy_safe = c->xy_safe ? 1 : 0;
+  p.xy_calc = c->xy_calc ? 1 : 0;
+  p.cx = c->cam[0];
+  p.cy = c->cam[1];
+  p.fx = c->cam[2];
+  p.fy = c->cam[3];
   p.nc_rays = c->d_nc;
   p.o0 = c->Oc[0];
   p.o1 = c->Oc[1];
