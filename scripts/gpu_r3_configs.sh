@@ -3,7 +3,7 @@
 # c3: the 36-view scan, strong scaling), each followed by rocprofv3
 # --kernel-trace --stats of the same command (no CPU baseline, no secondary
 # lines).  CONFIGS="c1 c3 ..." picks configs.  -> gpurun_out/r3cfg
-set -u
+set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=gpurun_out/r3cfg

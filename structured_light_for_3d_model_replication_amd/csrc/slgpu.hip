@@ -1762,8 +1762,10 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       // (9.5 + 9.5 kappa) u |P| < 2^7.3 u |P| < 2^8 f64 ulps of P for kappa
       // <= 16.  A coordinate whose 29 dropped mantissa bits lie within 2^13
       // ulps of the midpoint pattern 2^28, or outside 2^-100 <= |P'| < 2^100
-      // (zeros, signs of zero, inf / NaN), or a point with kappa > 16 or
-      // sum|n_i v_i| or |w| below 2^-500, goes to the operators' sequences below:
+      // (zeros, signs of zero, inf / NaN), or a point with kappa > 16 goes to
+      // the operators' sequences below (the host takes the route only for
+      // plane tables with |w| >= 2^-500 and max|n_i| >= 2^-400, so that
+      // sum|n_i v_i| >= 2^-420: planes_plain):
       // the stored float32 is the reference's bit for bit either way
       // (tests/test_gpu_parity.py compares the two routes).
       // (bitwise, not short-circuit: the tests stay branch-free VALU / SALU.
@@ -1774,9 +1776,8 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         const unsigned lo = static_cast<unsigned>(__double_as_longlong(v)) & 0x1fffffffu;
         return (lo - (0x10000000u - 8192u)) <= 16384u;
       };
-      auto out_of_range = [](double v) -> bool {
-        const unsigned ex = static_cast<unsigned>(static_cast<unsigned long long>(__double_as_longlong(v)) >> 52) & 0x7ffu;
-        return (ex - (1023u - 80u)) >= 160u;
+      auto out_of_range = [](double v) -> bool {  // not 2^-80 <= |v| < 2^80 (NaN included)
+        return !(fabs(v) >= 0x1p-80) | !(fabs(v) < 0x1p80);
       };
 #pragma unroll
       for (int i = 0; i < kPipe; ++i) {
@@ -1788,7 +1789,8 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         X[i] = x * q;
         Y[i] = y * q;
         Z[i] = q;
-        bool bad = (S > 16.0 * fabs(dv)) | !(S >= 0x1p-500) | !(fabs(pl[i].w) >= 0x1p-500) | out_of_range(Z[i]);
+        // (S >= 2^-420 and |w| >= 2^-500 hold for every point: planes_plain)
+        bool bad = (S > 16.0 * fabs(dv)) | out_of_range(Z[i]);
         if (pose) {
           // the turntable pose (the epilogue's order, below) on P': each output
           // k is within (161.5 + 8) u M_k of the epilogue on P_ref, M_k =
@@ -2096,6 +2098,7 @@ struct sl_ctx {
   bool xy_safe = false;     // every xn / yn table entry is div_safe (Params::xy_safe)
   bool xy_calc = false;     // xy_of reproduces every xn / yn entry (k_xy_check; SLGPU_XY_CALC=0: gathers, A/B)
   bool xy_plain = false;    // every xn / yn entry has 2^-20 <= |v| <= 2^20 (the verified route's range premise)
+  bool planes_plain = false;  // every plane has |w| >= 2^-500 and max|n_i| >= 2^-400 (ditto)
   bool xy_calc_env = true;
   double cam[4] = {0, 0, 1, 1};  // cx, cy, fx, fy
   bool verify32 = true;     // SL_XYZ_F32 by the verified shorter route (SLGPU_VERIFY32=0: the exact sequence, A/B)
@@ -2809,6 +2812,11 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
     for (int u = 0; u < W && ok; ++u) ok = plain(xn[u]);
     for (int v = 0; v < H && ok; ++v) ok = plain(yn[v]);
     c->xy_plain = ok;
+    ok = true;
+    for (int i = 0; i < Wp && ok; ++i)
+      ok = fabs(pl[4 * i + 3]) >= 0x1p-500 &&
+           std::max(fabs(pl[4 * i]), std::max(fabs(pl[4 * i + 1]), fabs(pl[4 * i + 2]))) >= 0x1p-400;
+    c->planes_plain = ok;
   }
   c->cam[0] = cx;
   c->cam[1] = cy;
@@ -2865,7 +2873,7 @@ static int xyz_mode_bits(const sl_ctx* c, int xyz_dtype, const double* poses) {
   if (xyz_dtype == SL_XYZ_F32_FAST && pinhole0 && !poses) return M_FAST32;
   // SL_XYZ_F32 (and F32_FAST where its bound does not apply): the verified
   // shorter f64 route where P = r t (Oc = 0, pinhole rays; with or without a pose)
-  return pinhole0 && c->verify32 && c->xy_plain ? M_VERIFY : nc_bit;
+  return pinhole0 && c->verify32 && c->xy_plain && c->planes_plain ? M_VERIFY : nc_bit;
 }
 
 static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
