@@ -506,7 +506,13 @@ def main():
         # this rank's K steps are complete here; the closing barrier's own
         # latency stays out of the interval (the max over ranks covers skew)
         el = time.perf_counter() - t0
-        us = [1e3 * evs[i].elapsed_time(evs[i + 1]) for i in range(k)] if evs else None
+        us = None
+        if evs:
+            # completion times from the window's first event; with several
+            # lanes (--streams) steps complete on different streams, so the
+            # per-step intervals are those of the sorted completion times
+            tc = sorted(evs[0].elapsed_time(evs[i + 1]) for i in range(k))
+            us = [1e3 * (b - a_) for a_, b in zip([0.0] + tc[:-1], tc)]
         return el, us
 
     def preroll(ms):
@@ -659,9 +665,10 @@ def main():
                        "stack_ready": bool(a.stack_ready)},
             "timing": {"preroll": pre,
                        "step_us": spread(step_us),
-                       "step_us_note": "HIP events at every step boundary, on the step's stream (completion to "
-                                       "completion), in an identical window right after the timed one (the events "
-                                       "add ~5.7 us of idle per step: not in the headline window)",
+                       "step_us_note": "HIP events at every step boundary, on the step's stream; intervals "
+                                       "between the sorted completion times (several lanes: steps complete on "
+                                       "different streams), in an identical window right after the timed one "
+                                       "(the events add ~5.7 us of idle per step: not in the headline window)",
                        "ms_per_step_with_events": 1e3 * el_ev / a.steps,
                        "gc": "collected before the pre-roll, disabled through the windows"},
             "roofline": {"bound": "hbm", "scope": "whole path per step: every kernel of the step",

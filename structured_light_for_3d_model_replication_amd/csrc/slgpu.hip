@@ -2465,9 +2465,10 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
         p.mode = decode_mode;
         void* args[] = {&p};
         c->last.p[1] = p;
-        c->last.fn[1] = reinterpret_cast<const void*>(k_stats);
+        const void* kst = reinterpret_cast<const void*>(k_stats);
+        c->last.fn[1] = kst;
         c->last.grid[1] = sg;
-        HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(k_stats), sg, dim3(kThreads), args, 0, ss));
+        HIP_TRY(c, hipLaunchKernel(kst, sg, dim3(kThreads), args, 0, ss));
         if (ahead) {
           HIP_TRY(c, hipEventRecord(c->stats_ev, ss));
           HIP_TRY(c, hipStreamWaitEvent(s, c->stats_ev, 0));
