@@ -64,8 +64,10 @@ CONFIGS = {
     "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0,
                streams=6),
     "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0),
-    "c3": dict(H=1080, W=1920, Wp=1920, Hp=1080, rows=True, views=36, maps=False, pose=False, deg=10.0),
-    "c4": dict(H=3000, W=4000, Wp=1920, Hp=1080, rows=True, views=45, maps=False, pose=False, deg=1.0),
+    "c3": dict(H=1080, W=1920, Wp=1920, Hp=1080, rows=True, views=36, maps=False, pose=False, deg=10.0,
+               streams=2),
+    "c4": dict(H=3000, W=4000, Wp=1920, Hp=1080, rows=True, views=45, maps=False, pose=False, deg=1.0,
+               streams=2),
     "c5": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=45, maps=False, pose=True, deg=1.0,
                streams=2),
 }
