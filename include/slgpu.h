@@ -40,7 +40,8 @@ extern "C" {
                              sl_system.py:553-554                                      */
 #define SL_EHIP (-3)      /* HIP runtime failure -> RuntimeError                        */
 #define SL_ENOCALIB (-4)  /* sl_set_calib not called / shape mismatch -> ValueError       */
-#define SL_ETIMEOUT (-5)  /* reserved (no device-side waits in this version)             */
+#define SL_ETIMEOUT (-5)  /* reserved (the one device-side wait, k_fused's bounded look-back,
+                             reports a give-up as a view_offsets total of -1)           */
 #define SL_ECAPACITY (-6) /* output capacity smaller than the pixel count -> ValueError   */
 #define SL_EIO (-7)       /* file could not be written -> OSError                        */
 
@@ -172,7 +173,8 @@ int sl_profile_enable(sl_ctx* ctx, int max_calls);
 int sl_profile_read(sl_ctx* ctx, double* decode_ms, double* count_ms, double* cloud_ms, int* calls);
 
 /* The last call's kernel path -- 0: k_decode + k_count + k_cloud; 1: [k_stats]
- * + k_decode + k_cloud, k_decode applying the mask and the point decision
+ * + k_decode + k_cloud, k_decode applying the mask and the point decision;
+ * 2: [k_stats] + k_fused (decode and cloud in one launch, SLGPU_FUSED=1)
  * (frames with W % 16 == 0, W, H <= 4096 and Wp <= 2048; sl_profile_* and
  * sl_time_kernels then report k_stats in the k_count slot) -- its number of
  * launch groups, and the pixels of its last launch group (what

@@ -121,6 +121,7 @@ constexpr int M_TEX = 2048;    // k_cloud: a BGR texture (else the white plane r
 constexpr int M_VERIFY = 4096; // k_cloud, SL_XYZ_F32: a shorter f64 evaluation whose f32 rounding is proven equal
                                // to the reference's (else the operators' sequences); Oc = 0, pinhole rays
                                // (with or without a pose)
+constexpr int M_FUSED = 1024;  // k_fused: k_decode's chunk group, then its cloud (look-back offsets) in one launch
 constexpr int M_DECIDE = 256;  // k_decode: also the mask and the |n.r| decision (k_count's work; k_stats
                                // histograms): mask map, point nibbles, chunk counts, block sums
 constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
@@ -220,6 +221,8 @@ struct Params {
   unsigned* super_zero;    // the next launch's super-block sums: zeroed by this launch's k_decode
   int super_cap;           // entries of each super buffer
   int sb_shift;
+  unsigned long long* lb;  // k_fused: look-back granules, one per workgroup of the launch (zeroed before it)
+  int64_t lb_n;            // ... their number (k_stats zeroes them)
 };
 
 // ---------------------------------------------------------------- helpers ----
@@ -484,6 +487,8 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p) {
   const int64_t HW = p.HW;
   if (blockIdx.x == 0)  // the next launch group's histograms of this slot (its scratch here)
     for (int i = tid; i < kHistView; i += kThreads) p.hist_zero[static_cast<int64_t>(view) * kHistView + i] = 0u;
+  if (p.lb && blockIdx.x == 0 && view == 0)  // k_fused's look-back granules (it follows this launch)
+    for (int64_t i = tid; i < p.lb_n; i += kThreads) p.lb[i] = 0ull;
   for (int i = tid; i < 256 * kHistStride; i += kThreads) s_hist[i] = 0u;
   __syncthreads();
   const uint8_t* vb = p.stack + view * p.stack_vs;
@@ -590,8 +595,15 @@ constexpr int kDecodePerCu = SLGPU_DECODE_PER_CU;  // default k_decode grid cap,
 #ifndef SLGPU_DECODE_WAVES
 #define SLGPU_DECODE_WAVES 3
 #endif
-template <int KC, int KR, int MODE, int VEC>
-__global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params p) {
+// k_decode's body; group_hook(col, pt, live, n_px, civ, cg, s_lds) runs at
+// the end of each chunk group when the mode has M_FUSED (k_fused: the
+// group's cloud in the same launch), else nothing.
+struct NoGroupHook {
+  template <class... A>
+  __device__ void operator()(A&&...) const {}
+};
+template <int KC, int KR, int MODE, int VEC, class Hook>
+__device__ __forceinline__ void decode_body(const Params& p, const Hook& group_hook) {
   const int mode = MODE >= 0 ? MODE : p.mode;
   const int kc = KC >= 0 ? KC : p.kc;
   const int krr = (mode & M_ROWS) ? (KR >= 0 ? KR : p.kr) : 0;
@@ -954,7 +966,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
     }
   }
 
-  if ((mode & M_CODES) && !p.rec_col) {
+  if ((mode & M_CODES) && !p.rec_col && !(mode & M_FUSED)) {
     // records for k_count / k_cloud: clipped column code
     uint32_t rec[kPx / 2];
 #pragma unroll
@@ -988,7 +1000,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
         if (k < n_px) p.codes[o + k] = static_cast<uint16_t>(rec[k >> 1] >> (16 * (k & 1)));
     }
   }
-  if (decide && (mode & M_CODES) && !p.bs_atomic) {  // the workgroup's block sum (k_count's, for k_cloud's offsets)
+  if (decide && (mode & M_CODES) && !p.bs_atomic && !(mode & M_FUSED)) {  // the workgroup's block sum (k_count's, for k_cloud's offsets)
     __syncthreads();
     if (tid == 0) {
       int t = 0;
@@ -999,6 +1011,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
       if (t) atomicAdd(p.super_sums + (blk >> p.sb_shift), static_cast<unsigned>(t));
     }
   }
+  if (mode & M_FUSED) group_hook(col, pt_rec, live, n_px, civ, cg, s_lds);
   ++it;
   }  // chunk groups
 
@@ -1025,6 +1038,11 @@ __global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params 
       if (m > -1024) atomicMax(gh + 256, static_cast<unsigned>(m + 1024));
     }
   }
+}
+
+template <int KC, int KR, int MODE, int VEC>
+__global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params p) {
+  decode_body<KC, KR, MODE, VEC>(p, NoGroupHook{});
 }
 
 // ================================================================= k_count ====
@@ -1772,12 +1790,12 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       // The host takes this route only when every table x, y has 2^-20 <=
       // |x|, |y| <= 2^20 (xy_plain), so 2^-80 <= |Z| < 2^80 puts X, Y and Z
       // in 2^-100 .. 2^100: normal float32 values, no zeros)
-      auto ambiguous = [](double v) -> bool {
+      auto ambiguous = [](double v) -> unsigned {
         const unsigned lo = static_cast<unsigned>(__double_as_longlong(v)) & 0x1fffffffu;
         return (lo - (0x10000000u - 8192u)) <= 16384u;
       };
-      auto out_of_range = [](double v) -> bool {  // not 2^-80 <= |v| < 2^80 (NaN included)
-        return !(fabs(v) >= 0x1p-80) | !(fabs(v) < 0x1p80);
+      auto out_of_range = [](double v) -> unsigned {  // not 2^-80 <= |v| < 2^80 (NaN included)
+        return static_cast<unsigned>(!(fabs(v) >= 0x1p-80)) | static_cast<unsigned>(!(fabs(v) < 0x1p80));
       };
 #pragma unroll
       for (int i = 0; i < kPipe; ++i) {
@@ -1790,7 +1808,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         Y[i] = y * q;
         Z[i] = q;
         // (S >= 2^-420 and |w| >= 2^-500 hold for every point: planes_plain)
-        bool bad = (S > 16.0 * fabs(dv)) | out_of_range(Z[i]);
+        unsigned bad = static_cast<unsigned>(S > 16.0 * fabs(dv)) | out_of_range(Z[i]);
         if (pose) {
           // the turntable pose (the epilogue's order, below) on P': each output
           // k is within (161.5 + 8) u M_k of the epilogue on P_ref, M_k =
@@ -1799,11 +1817,11 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           // point is settled when float32(v - B) == float32(v + B), B =
           // 2^-44 M_k, a normal float32 (then the reference's value, inside
           // that interval, has the same float32)
-          auto unsettled = [](double v, double m) -> bool {
+          auto unsettled = [](double v, double m) -> unsigned {
             const double B = m * 0x1p-44;
             const uint32_t a = __float_as_uint(static_cast<float>(v - B));
             const uint32_t b = __float_as_uint(static_cast<float>(v + B));
-            return (a != b) | (((a >> 23) & 0xffu) - 1u >= 254u);
+            return static_cast<unsigned>(a != b) | static_cast<unsigned>(((a >> 23) & 0xffu) - 1u >= 254u);
           };
           const double x0 = X[i], x1 = Y[i], x2 = Z[i];
           const double X2 = ((pm[0] * x0 + pm[1] * x1) + pm[2] * x2) + pm[3];
@@ -1819,7 +1837,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         } else {
           bad |= ambiguous(X[i]) | ambiguous(Y[i]) | ambiguous(Z[i]);
         }
-        slow |= static_cast<uint32_t>(bad) << i;
+        slow |= (bad & 1u) << i;
       }
     }
     // The kPipe points' chains (sqrt, shared reciprocal, divisions) carry no
@@ -2079,6 +2097,116 @@ __global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : SLGPU_CLOUD_WAVES) voi
   cloud_chunk<MODE, VEC, PIPE>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0]);
 }
 
+// ================================================================= k_fused ====
+// k_decode + k_cloud in one launch for calls of one launch group
+// (SLGPU_FUSED=1, measured A/B): every workgroup decodes its chunk group as
+// k_decode does (maps, mask, decision; no records), then, after a decoupled
+// look-back over the workgroups before it for its output offset, triangulates
+// its own points from registers -- the codes never leave the chip and one
+// kernel boundary goes.  The look-back waits only on lower-numbered
+// workgroups, dispatched before it and waiting on none after them, so it
+// completes whatever the residency (other calls in flight included); its
+// spin is bounded all the same (a give-up writes -1 as the call's total).
+// Granules (Params::lb): 8 bytes {tag, value}, stored and loaded whole at
+// agent scope -- the data is the flag (tag 1: the block's own count, 2: the
+// inclusive prefix) -- zeroed before the launch (k_stats, or a memset).
+__device__ __forceinline__ long long lookback_prefix(const Params& p, int64_t blk, unsigned own, int lane,
+                                                     bool* failed) {
+  unsigned long long* lb = p.lb;
+  if (lane == 0)
+    __hip_atomic_store(lb + blk, ((blk == 0 ? 2ull : 1ull) << 32) | own, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  *failed = false;
+  if (blk == 0) return 0;
+  long long acc = 0;
+  int64_t j = blk - 1;  // lane k reads block j - k
+  for (unsigned spins = 0;;) {
+    const int64_t jj = j - lane;
+    const unsigned long long g =
+        jj >= 0 ? __hip_atomic_load(lb + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (2ull << 32);
+    const unsigned tag = static_cast<unsigned>(g >> 32);
+    const unsigned long long incl = __ballot(tag == 2u);
+    const unsigned long long ready = __ballot(tag != 0u);
+    const int f = incl ? __builtin_ctzll(incl) : 63;  // the nearest inclusive prefix (or the whole window)
+    const unsigned long long need = f == 63 ? ~0ull : ((2ull << f) - 1ull);
+    if ((ready & need) == need) {
+      acc += wave_sum64(lane <= f ? static_cast<long long>(static_cast<unsigned>(g)) : 0ll);
+      if (incl) break;
+      j -= 64;
+      continue;
+    }
+    if (++spins > (1u << 22)) {  // never expected (see above): give up rather than hang
+      *failed = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (lane == 0)
+    __hip_atomic_store(lb + blk, (2ull << 32) | static_cast<unsigned>(acc + own), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return acc;
+}
+
+template <int KC, int KR, int MODE, int CMODE, int PIPE>
+__global__ __launch_bounds__(kThreads, 2) void k_fused(Params p) {
+  __shared__ long long s_base;
+  __shared__ int s_wc[kWaves];
+  __shared__ int s_fail;
+  static_assert((MODE & M_FUSED) && (MODE & M_DECIDE) && (MODE & M_CODES), "k_fused: a decide-path cloud call");
+  static_assert(kWaves * (kChunk + kBgrWords) * 4 <= kDecodeLds, "the cloud's LDS fits in the decode tables'");
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto group = [&](const uint32_t* col, uint32_t pt, bool live, int n_px, int civ, int cg, unsigned* s_lds) {
+    const int view = blockIdx.y;
+    const int64_t px0 = static_cast<int64_t>(civ) * kChunk + lane * kPx;
+    const int64_t pxl = (live && n_px > 0) ? px0 : 0;
+    ChunkIn in;
+    // the colour first: its latency overlaps the look-back
+    if (p.tex != nullptr) {
+      const uint8_t* t = p.tex + view * p.tex_vs + 3 * pxl;
+      in.tq[0] = ld_side16(t);
+      in.tq[1] = ld_side16(t + 16);
+      in.tq[2] = ld_side16(t + 32);
+    } else {
+      in.tq[0] = ld16(p.stack + view * p.stack_vs + pxl, n_px, true);
+      in.tq[1] = in.tq[2] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    const uint32_t cmax = static_cast<uint32_t>(p.Wp - 1);
+#pragma unroll
+    for (int i = 0; i < kPx / 2; ++i) in.d[i] = min(col[2 * i], cmax) | (min(col[2 * i + 1], cmax) << 16);
+    in.ptbits = (live && n_px == kPx) ? (pt & 0xffffu) : 0u;
+    const int cnt = wave_sum(__popc(in.ptbits));
+    if (lane == 0) s_wc[wid] = cnt;
+    __syncthreads();  // (also: every wave's decision is done with the LDS tables, reused below)
+    if (wid == 0) {
+      const int64_t blk = static_cast<int64_t>(view) * gridDim.x + cg;  // dispatch order
+      const unsigned own = static_cast<unsigned>(s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3]);
+      bool failed;
+      const long long pre = lookback_prefix(p, blk, own, lane, &failed);
+      if (lane == 0) {
+        s_base = pre + (p.base_in ? *p.base_in : 0ll);
+        s_fail = failed ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    long long base = s_base;
+    for (int w = 0; w < wid; ++w) base += s_wc[w];
+    base = uniform64(base);
+    if (s_fail && tid == 0) p.view_offsets[p.n_views] = -1;  // (the give-up: an invalid total)
+    if (live) {
+      if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1 && !s_fail) p.view_offsets[p.n_views] = base + cnt;
+      const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
+      uint32_t* s_ent = s_lds + wid * kChunk;
+      uint32_t* s_bgr = s_lds + kWaves * kChunk + wid * kBgrWords;
+      float dummy_xyz[1];
+      uint8_t dummy_col[4];
+      cloud_chunk<CMODE, 1, PIPE>(p, gc, base, lane, in, s_ent, s_bgr, dummy_xyz, dummy_col);
+    }
+  };
+  decode_body<KC, KR, MODE, 1>(p, group);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ host ----
@@ -2159,12 +2287,16 @@ struct sl_ctx {
   bool ready_next = false;        // sl_stack_ready: armed for the next sl_decode_triangulate
   hipEvent_t ready_ev_next = nullptr;
   bool no_side = false;           // SLGPU_STATS_SIDE=0: k_stats always on the call's stream (A/B)
+  bool fused = false;             // SLGPU_FUSED=1: k_fused for one-group cloud calls (A/B)
+  unsigned long long* d_lb = nullptr;  // k_fused's look-back granules
+  int64_t cap_lb = 0;
   bool side_groups = false;       // SLGPU_STATS_SIDE=1: also the later launch groups of every call (A/B;
                                   // off by default: a cross-stream event wait measured 10-20 us of latency,
                                   // more than the k_stats it hides)
   struct {
     bool valid = false;
     bool decide = false;  // fn[1] = k_stats (or null) instead of k_count
+    bool fused = false;   // fn[0] = k_fused (decode and cloud), fn[2] = null
     Params p[3];
     const void* fn[3] = {nullptr, nullptr, nullptr};  // k_decode, k_count, k_cloud (or null)
     dim3 grid[3];
@@ -2329,6 +2461,18 @@ KernelFn pick_cloud(int mode, bool vec, bool small) {
   return vec ? k_cloud<-1, 1, kExactPipe> : k_cloud<-1, 0, kExactPipe>;  // (f64 chains: kExactPipe points per pass)
 }
 
+// k_fused instantiations: the benchmark configurations' one-group calls
+// (decode mode with M_DECIDE | M_FUSED, cloud mode), else null
+KernelFn pick_fused(int kc, int kr, int dmode, int cmode) {
+  constexpr int D = M_DECIDE | M_FUSED, mrch = M_MAPS | M_ROWS | M_CODES | M_HIST, ch = M_CODES | M_HIST;
+  constexpr int V = M_VERIFY | M_TEX, F = M_FAST32 | M_TEX;
+  if (dmode == (mrch | D) && kc == 10 && kr == 0 && cmode == V) return k_fused<10, 0, mrch | D, V, kVerifyPipe>;
+  if (dmode == (mrch | D) && kc == 11 && kr == 11 && cmode == V) return k_fused<11, 11, mrch | D, V, kVerifyPipe>;
+  if (dmode == (mrch | D) && kc == 11 && kr == 11 && cmode == F) return k_fused<11, 11, mrch | D, F, kPipe>;
+  if (dmode == (ch | D) && kc == 11 && cmode == V) return k_fused<11, 0, ch | D, V, kVerifyPipe>;
+  return nullptr;
+}
+
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // Enqueue, per launch group of views, k_decode -> k_count [-> k_cloud] on
@@ -2456,6 +2600,19 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     c->last.s = s;
     c->last.fn[2] = nullptr;
     c->last.decide = decide;
+    // k_fused (SLGPU_FUSED=1): a one-group cloud call's decode and cloud in
+    // one launch; its look-back granules zeroed by k_stats (or a memset)
+    KernelFn fusedfn = nullptr;
+    if (c->fused && decide && vec && cloud_mode >= 0 && n_groups == 1)
+      fusedfn = pick_fused(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode | M_FUSED, cloud_mode);
+    c->last.fused = fusedfn != nullptr;
+    if (fusedfn) {
+      r = grow(c, &c->d_lb, &c->cap_lb, static_cast<int64_t>(grid.x) * nv);
+      if (r) return r;
+      p.lb = c->d_lb;
+      p.lb_n = static_cast<int64_t>(grid.x) * nv;
+      if (!adaptive) HIP_TRY(c, hipMemsetAsync(c->d_lb, 0, sizeof(unsigned long long) * p.lb_n, s));
+    }
     if (decide) {
       c->last.fn[1] = nullptr;
       if (adaptive) {  // k_stats: the thresholds' histograms, before the decode applies them
@@ -2476,7 +2633,16 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       }
       if (gev) HIP_TRY(c, hipEventRecord(gev[1], s));
     }
-    {
+    if (fusedfn) {  // one workgroup per chunk group (uncapped grid), then its cloud
+      p.mode = decode_mode | M_FUSED;
+      p.bs_atomic = 0;
+      void* args[] = {&p};
+      c->last.p[0] = p;
+      c->last.p[0].masked = nullptr;
+      c->last.fn[0] = reinterpret_cast<const void*>(fusedfn);
+      c->last.grid[0] = grid;
+      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fusedfn), grid, dim3(kThreads), args, 0, s));
+    } else {
       p.mode = decode_mode;
       void* args[] = {&p};
       KernelFn fn = pick_decode(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode, vec);
@@ -2501,7 +2667,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       if (adaptive && c->hist_tracked) HIP_TRY(c, hipEventRecord(c->hist_ev, s));  // k_count reads them too
     }
     if (gev && !decide) HIP_TRY(c, hipEventRecord(gev[2], s));
-    if (cloud_mode >= 0) {
+    if (cloud_mode >= 0 && !fusedfn) {
       p.mode = cloud_mode;
       void* args[] = {&p};
       // at most one chunk per SIMD: all of a chunk's points in one pass
@@ -2682,6 +2848,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
     c->side_groups = atoi(d) == 1;
   }
   if (const char* d = getenv("SLGPU_XY_CALC")) c->xy_calc_env = atoi(d) != 0;
+  if (const char* d = getenv("SLGPU_FUSED")) c->fused = atoi(d) != 0;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
@@ -2710,7 +2877,8 @@ void sl_ctx_destroy(sl_ctx* c) {
                     static_cast<void*>(c->d_codes), static_cast<void*>(c->d_hist[0]),
                     static_cast<void*>(c->d_hist[1]), static_cast<void*>(c->d_ptnib),
                     static_cast<void*>(c->d_block_sums), static_cast<void*>(c->d_chunk_counts),
-                    static_cast<void*>(c->d_super[0]), static_cast<void*>(c->d_super[1])})
+                    static_cast<void*>(c->d_super[0]), static_cast<void*>(c->d_super[1]),
+                    static_cast<void*>(c->d_lb)})
     if (ptr) (void)hipFree(ptr);
   delete c;
 }
@@ -3136,7 +3304,7 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
 
 int sl_last_launch_info(sl_ctx* c, int* path, int64_t* launches, int64_t* last_launch_px) {
   if (!c) return SL_EINVAL;
-  if (path) *path = c->last.decide ? 1 : 0;
+  if (path) *path = c->last.fused ? 2 : c->last.decide ? 1 : 0;
   if (launches) *launches = c->last_launches;
   if (last_launch_px) *last_launch_px = c->last_launch_px;
   return SL_OK;
