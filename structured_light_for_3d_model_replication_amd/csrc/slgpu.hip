@@ -1747,7 +1747,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         int uu, vv;
         chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
         if (kXyCalc && p.xy_calc) {  // (uniform) the table values, computed: no 16 B of gathers per point
-          ra[i] = xy_of(uu, p.cx, p.fx);
+          ra[i] = xy_of(uu, p.cx, p.fx);  // (gathering x or y instead: +0.8 / +1.1 us at c2)
           rb[i] = xy_of(vv, p.cy, p.fy);
         } else {
           ra[i] = p.xn[uu];
