@@ -143,6 +143,22 @@ int sl_mask_counts_to(sl_ctx* ctx, int64_t* device_counts);
  * Not applied while the call's stream is being captured into a graph. */
 int sl_stack_ready(sl_ctx* ctx, void* event);
 
+/* A prepared call: sl_decode_triangulate's arguments (without the stream),
+ * checked once and kept, so that a stream of views through the same resident
+ * buffers (a ring of stack slots, reused outputs) re-enqueues it with two
+ * arguments -- what a host-bound caller of small frames spends its time on is
+ * the per-call argument marshalling, not the kernels.  sl_call_run is exactly
+ * sl_decode_triangulate with the kept arguments on `stream` (the same checks,
+ * results and errors); the buffers must stay valid until sl_call_destroy. */
+typedef struct sl_call sl_call;
+int sl_call_prepare(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_stride, int n_views, int n_img,
+                    int H, int W, int n_cols, int n_rows, const uint8_t* tex_bgr, int64_t tex_view_stride,
+                    int mask_mode, const double* poses, int32_t* col_out, int32_t* row_out, uint8_t* mask_out,
+                    void* xyz_out, int xyz_dtype, uint8_t* bgr_out, int64_t out_capacity, int64_t* view_offsets,
+                    sl_call** out);
+int sl_call_run(sl_call* call, void* stream);
+void sl_call_destroy(sl_call* call);
+
 /* reconstruct_point_cloud on caller-supplied maps (sl_system.py:584-653).
  * col_map device int32 [n_views][H][W]; mask device uint8 [n_views][H][W]
  * (non-zero = valid); tex_bgr device [n_views][H][W][3].  Outputs as above. */

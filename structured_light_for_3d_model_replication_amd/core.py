@@ -184,6 +184,28 @@ class Reconstructor:
         stream beside the previous call's triangulation (sl_stack_ready).
         Results are unchanged.
         """
+        args, res, keep, (V, H, W, cloud) = self._resolve(stack, n_cols, n_rows, texture, mask_mode, maps, cloud,
+                                                         xyz_dtype, poses, fast_f32, out)
+        if mask_counts is not None and (mask_counts.dtype != torch.int64 or mask_counts.device != self.device
+                                        or mask_counts.numel() < V or not mask_counts.is_contiguous()):
+            raise ValueError(f"mask_counts must be a contiguous int64 tensor of >= {V} entries on {self.device}")
+        with self._lock:
+            if cloud and (self._H, self._W) != (H, W):
+                raise ValueError(f"calibration is for {self._W}x{self._H}, stack is {W}x{H}")
+            if mask_counts is not None:
+                _lib.check(self._L.sl_mask_counts_to(self._ctx, mask_counts.data_ptr()), self._ctx,
+                           "sl_mask_counts_to")
+            if stack_ready is not None and stack_ready is not False:
+                ev = None if stack_ready is True else ctypes.c_void_p(stack_ready.cuda_event)
+                _lib.check(self._L.sl_stack_ready(self._ctx, ev), self._ctx, "sl_stack_ready")
+            _lib.check(self._L.sl_decode_triangulate(self._ctx, *args, self._stream(stream)), self._ctx,
+                       "sl_decode_triangulate")
+        return res
+
+    def _resolve(self, stack, n_cols, n_rows, texture, mask_mode, maps, cloud, xyz_dtype, poses, fast_f32, out):
+        """decode_triangulate's argument checks and output buffers -> (the
+        C-ABI arguments after the context and before the stream, the result
+        dict, tensors to keep alive, (V, H, W, cloud))."""
         if stack.dtype != torch.uint8 or stack.device != self.device:
             raise ValueError("stack must be a uint8 tensor on the reconstructor's device")
         if stack.dim() == 3:
@@ -225,29 +247,34 @@ class Reconstructor:
             bgr, vo = out["bgr"], out["view_offsets"]
             if vo.shape[0] != V + 1:
                 vo = out["view_offsets"] = torch.empty(V + 1, dtype=torch.int64, device=self.device)
-        if mask_counts is not None and (mask_counts.dtype != torch.int64 or mask_counts.device != self.device
-                                        or mask_counts.numel() < V or not mask_counts.is_contiguous()):
-            raise ValueError(f"mask_counts must be a contiguous int64 tensor of >= {V} entries on {self.device}")
-        with self._lock:
-            if cloud and (self._H, self._W) != (H, W):
-                raise ValueError(f"calibration is for {self._W}x{self._H}, stack is {W}x{H}")
-            if mask_counts is not None:
-                _lib.check(self._L.sl_mask_counts_to(self._ctx, mask_counts.data_ptr()), self._ctx,
-                           "sl_mask_counts_to")
-            if stack_ready is not None and stack_ready is not False:
-                ev = None if stack_ready is True else ctypes.c_void_p(stack_ready.cuda_event)
-                _lib.check(self._L.sl_stack_ready(self._ctx, ev), self._ctx, "sl_stack_ready")
-            _lib.check(self._L.sl_decode_triangulate(
-                self._ctx, stack.data_ptr(), stack.stride(0), V, n_img, H, W, int(n_cols), int(n_rows),
+        args = (stack.data_ptr(), stack.stride(0), V, n_img, H, W, int(n_cols), int(n_rows),
                 _ptr(texture), 3 * H * W if texture is None else texture.stride(0), MASK_MODES[mask_mode],
                 _ptr(poses), _ptr(col), _ptr(row), _ptr(msk), _ptr(xyz), xyz_code, _ptr(bgr),
-                cap if cloud else 0, _ptr(vo), self._stream(stream)), self._ctx, "sl_decode_triangulate")
+                cap if cloud else 0, _ptr(vo))
         res = {}
         if maps:
             res["col_map"], res["row_map"], res["mask"] = col, row, msk.view(torch.bool)
         if cloud:
             res["cloud"] = Cloud(xyz, bgr, vo)
-        return res
+        return args, res, (stack, texture, poses), (V, H, W, cloud)
+
+    def prepare(self, stack: torch.Tensor, n_cols: int = 1920, n_rows: int = 1080, *,
+                texture: torch.Tensor | None = None, mask_mode: str = "adaptive", maps: bool = False,
+                cloud: bool = True, xyz_dtype=torch.float32, poses: torch.Tensor | None = None,
+                fast_f32: bool = False, out: dict | None = None) -> "PreparedCall":
+        """decode_triangulate's arguments checked and bound once
+        (sl_call_prepare): ``PreparedCall.run(stream)`` re-enqueues the same
+        call -- the same stack buffer (refilled by the caller, e.g. a ring of
+        resident stack slots), the same output buffers -- for the cost of one
+        two-argument C call.  The result dict is ``PreparedCall.res``."""
+        args, res, keep, (V, H, W, cloud) = self._resolve(stack, n_cols, n_rows, texture, mask_mode, maps, cloud,
+                                                         xyz_dtype, poses, fast_f32, out)
+        with self._lock:
+            if cloud and (self._H, self._W) != (H, W):
+                raise ValueError(f"calibration is for {self._W}x{self._H}, stack is {W}x{H}")
+            h = ctypes.c_void_p()
+            _lib.check(self._L.sl_call_prepare(self._ctx, *args, ctypes.byref(h)), self._ctx, "sl_call_prepare")
+        return PreparedCall(self, h, res, keep)
 
     def triangulate_maps(self, col_map: torch.Tensor, mask: torch.Tensor, texture: torch.Tensor, *,
                          xyz_dtype=torch.float64, poses=None, fast_f32: bool = False, stream=None) -> Cloud:
@@ -411,6 +438,35 @@ def engine(device=None) -> Reconstructor:
         return _engines[idx]
 
 
+class PreparedCall:
+    """A bound decode_triangulate (Reconstructor.prepare): ``run(stream)``
+    enqueues it again; ``res`` holds its outputs (overwritten by every run)."""
+
+    def __init__(self, eng: Reconstructor, handle, res: dict, keep):
+        self.eng, self._h, self.res, self._keep = eng, handle, res, keep
+        self._run = eng._L.sl_call_run
+
+    def run(self, stream=None) -> dict:
+        eng = self.eng
+        s = (stream if stream is not None else torch.cuda.current_stream(eng.device)).cuda_stream
+        with eng._lock:
+            rc = self._run(self._h, s)
+        if rc:
+            _lib.check(rc, eng._ctx, "sl_call_run")
+        return self.res
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.eng._L.sl_call_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
 class ReconstructorPool:
     """Views in flight on one GPU: ``lanes`` Reconstructors (own scratch, own
     outputs), each on its own HIP stream; successive ``decode_triangulate``
@@ -441,6 +497,7 @@ class ReconstructorPool:
         self.streams = [torch.cuda.Stream(self.device) for _ in range(lanes)]
         self._outs = [{} if reuse_outputs else None for _ in range(lanes)]
         self._keys = [None] * lanes  # a lane's last output shapes (reused buffers: no allocation)
+        self._plans = [None] * lanes  # a lane's prepared call and its argument key (resident inputs)
         self._next = 0
         self._lock = threading.Lock()
 
@@ -466,8 +523,6 @@ class ReconstructorPool:
         caller knows are ready and kept alive (e.g. resident stacks)."""
         if "stream" in kw:
             raise ValueError("ReconstructorPool picks the stream (one per lane)")
-        if not wait_inputs:
-            kw.setdefault("stack_ready", True)  # the caller's promise covers the histogram pass too
         with self._lock:
             i = self._next
             self._next = (i + 1) % len(self.engines)
@@ -477,6 +532,27 @@ class ReconstructorPool:
             for t in (stack, kw.get("texture"), kw.get("poses")):
                 if isinstance(t, torch.Tensor) and t.is_cuda:
                     t.record_stream(st)  # the caller may free it before the lane has read it
+        if not wait_inputs and self._outs[i] is not None and kw.get("out") is None and \
+                kw.get("mask_counts") is None and not kw.get("stack_ready"):
+            # resident inputs into reused outputs: a prepared call per lane and
+            # argument set (sl_call_prepare), re-run with one two-argument call
+            tex, pos = kw.get("texture"), kw.get("poses")
+            pkey = (stack.data_ptr(), stack.shape, n_cols, n_rows, None if tex is None else tex.data_ptr(),
+                    None if pos is None else pos.data_ptr(), kw.get("maps", False), kw.get("cloud", True),
+                    kw.get("xyz_dtype", torch.float32), kw.get("fast_f32", False), kw.get("mask_mode", "adaptive"))
+            plan = self._plans[i]
+            if plan is None or plan[0] != pkey:
+                pk = {k: v for k, v in kw.items() if k not in ("mask_counts", "stack_ready")}
+                with torch.cuda.stream(st):  # outputs (re)allocated here belong to the lane stream
+                    pc = eng.prepare(stack, n_cols, n_rows, out=self._outs[i], **pk)
+                if plan is not None:
+                    plan[1].close()
+                plan = self._plans[i] = (pkey, pc)
+                self._keys[i] = None
+            res = dict(plan[1].run(st))
+            res["stream"] = st
+            res["lane"] = i
+            return res
         key = None
         if self._outs[i] is not None and kw.get("out") is None:
             kw["out"] = self._outs[i]
@@ -500,5 +576,9 @@ class ReconstructorPool:
             e.sync(st)
 
     def close(self) -> None:
+        for k, plan in enumerate(self._plans):
+            if plan is not None:
+                plan[1].close()
+                self._plans[k] = None
         for e in self.engines:
             e.close()

@@ -190,6 +190,7 @@ struct Params {
   int xy_calc;             // k_cloud computes xn / yn (xy_of) instead of gathering them: sl_set_calib
                            // checked on the device that xy_of gives every table entry bit for bit
   double cx, cy, fx, fy;   // cam_K's (sl_system.py:610-611), for xy_of
+  double rfx, rfy;         // fl(1 / fx), fl(1 / fy): the verified route's x, y
   const double* nc_rays;   // Nc table [3][HW] or null
   double o0, o1, o2;       // Oc
   const double* poses;
@@ -1746,7 +1747,13 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       } else {
         int uu, vv;
         chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
-        if (kXyCalc && p.xy_calc) {  // (uniform) the table values, computed: no 16 B of gathers per point
+        if (mode & M_VERIFY) {
+          // the verified route's x, y: (w - c) * fl(1 / f), within 3 u of the
+          // table values (its error bound allows it; the
+          // fallback re-reads the tables)
+          ra[i] = (static_cast<double>(uu) - p.cx) * p.rfx;
+          rb[i] = (static_cast<double>(vv) - p.cy) * p.rfy;
+        } else if (kXyCalc && p.xy_calc) {  // (uniform) the table values, computed: no 16 B of gathers per point
           ra[i] = xy_of(uu, p.cx, p.fx);  // (gathering x or y instead: +0.8 / +1.1 us at c2)
           rb[i] = xy_of(vv, p.cy, p.fy);
         } else {
@@ -1776,9 +1783,9 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       // and P_ref.  Error bound (u = 2^-53, kappa = sum|n_i v_i| / |n . v| =
       // sum|n_i r_i| / |n . r|): the reference's chain (s2: 3u, |v|: 2.5u,
       // r: 3.5u, den: 6.5u kappa, t: +u, P: +u) is within (5.5 + 6.5 kappa) u
-      // |P| of the exact P, P' within (4 + 3 kappa) u |P|, so |P' - P_ref| <=
-      // (9.5 + 9.5 kappa) u |P| < 2^7.3 u |P| < 2^8 f64 ulps of P for kappa
-      // <= 16.  A coordinate whose 29 dropped mantissa bits lie within 2^13
+      // |P| of the exact P; P' (its x, y within 3u of the tables', below)
+      // within (7 + 6 kappa) u |P|, so |P' - P_ref| <= (12.5 + 12.5 kappa) u
+      // |P| < 2^7.8 u |P| < 2^8 f64 ulps of P for kappa <= 16.  A coordinate whose 29 dropped mantissa bits lie within 2^13
       // ulps of the midpoint pattern 2^28, or outside 2^-100 <= |P'| < 2^100
       // (zeros, signs of zero, inf / NaN), or a point with kappa > 16 goes to
       // the operators' sequences below (the host takes the route only for
@@ -1811,9 +1818,9 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         unsigned bad = static_cast<unsigned>(S > 16.0 * fabs(dv)) | out_of_range(Z[i]);
         if (pose) {
           // the turntable pose (the epilogue's order, below) on P': each output
-          // k is within (161.5 + 8) u M_k of the epilogue on P_ref, M_k =
-          // sum_j |m_kj P_j| + |m_k3| (P' within 161.5 u |P_j| per coordinate,
-          // the two evaluations' roundings 4 u M_k each) < 2^-45.6 M_k; the
+          // k is within (212.5 + 8) u M_k of the epilogue on P_ref, M_k =
+          // sum_j |m_kj P_j| + |m_k3| (P' within 212.5 u |P_j| per coordinate,
+          // the two evaluations' roundings 4 u M_k each) < 2^-45.2 M_k; the
           // point is settled when float32(v - B) == float32(v + B), B =
           // 2^-44 M_k, a normal float32 (then the reference's value, inside
           // that interval, has the same float32)
@@ -3067,6 +3074,8 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.cy = c->cam[1];
   p.fx = c->cam[2];
   p.fy = c->cam[3];
+  p.rfx = 1.0 / c->cam[2];
+  p.rfy = 1.0 / c->cam[3];
   p.nc_rays = c->d_nc;
   p.o0 = c->Oc[0];
   p.o1 = c->Oc[1];
@@ -3159,6 +3168,49 @@ int sl_stack_ready(sl_ctx* c, void* event) {
   c->ready_ev_next = static_cast<hipEvent_t>(event);
   return SL_OK;
 }
+
+// A prepared sl_decode_triangulate: its arguments, kept for sl_call_run.
+struct sl_call {
+  sl_ctx* c;
+  const uint8_t* stack;
+  int64_t stack_vs;
+  int n_views, n_img, H, W, n_cols, n_rows;
+  const uint8_t* tex;
+  int64_t tex_vs;
+  int mask_mode;
+  const double* poses;
+  int32_t* col_out;
+  int32_t* row_out;
+  uint8_t* mask_out;
+  void* xyz;
+  int xyz_dtype;
+  uint8_t* bgr;
+  int64_t cap;
+  int64_t* view_offsets;
+};
+
+int sl_call_prepare(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int n_views, int n_img, int H, int W,
+                    int n_cols, int n_rows, const uint8_t* tex, int64_t tex_vs, int mask_mode, const double* poses,
+                    int32_t* col_out, int32_t* row_out, uint8_t* mask_out, void* xyz, int xyz_dtype,
+                    uint8_t* bgr, int64_t cap, int64_t* view_offsets, sl_call** out) {
+  if (!c || !out) return SL_EINVAL;
+  *out = nullptr;
+  int r = common_out_checks(c, n_views, H, W, xyz, xyz_dtype, bgr, cap, view_offsets);
+  if (r) return r;
+  if (!stack) return fail(c, SL_EINVAL, "stack is NULL");
+  *out = new sl_call{c, stack, stack_vs, n_views, n_img, H, W, n_cols, n_rows, tex, tex_vs, mask_mode, poses,
+                     col_out, row_out, mask_out, xyz, xyz_dtype, bgr, cap, view_offsets};
+  return SL_OK;
+}
+
+int sl_call_run(sl_call* k, void* stream) {
+  if (!k) return SL_EINVAL;
+  return sl_decode_triangulate(k->c, k->stack, k->stack_vs, k->n_views, k->n_img, k->H, k->W, k->n_cols, k->n_rows,
+                               k->tex, k->tex_vs, k->mask_mode, k->poses, k->col_out, k->row_out, k->mask_out,
+                               k->xyz, k->xyz_dtype, k->bgr, k->cap, k->view_offsets, stream);
+}
+
+void sl_call_destroy(sl_call* k) { delete k; }
 
 int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, const uint8_t* tex,
                         int n_views, int H, int W, const double* poses, void* xyz, int xyz_dtype,
