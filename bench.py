@@ -119,6 +119,10 @@ def parse(argv=None):
                          "starts on a side stream beside the previous call's k_cloud; measured slower at c2, "
                          "DESIGN.md 5.2)")
     ap.add_argument("--no-stack-ready", dest="stack_ready", action="store_false")
+    ap.add_argument("--next-stats", dest="next_stats", action="store_true", default=True,
+                    help="every call names the next call's (resident) stack (sl_stack_next): its triangulation "
+                         "kernel also computes the next call's adaptive-mask histograms (default)")
+    ap.add_argument("--no-next-stats", dest="next_stats", action="store_false")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r03_traffic_c2.json"),
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
                          "scripts/traffic_from_pmc.py)")
@@ -450,9 +454,15 @@ def main():
     # histogram pass may start beside the previous call's k_cloud
     ready = True if a.stack_ready else None
 
+    # --next-stats (default): the next step reads the same resident stack, and
+    # each call names it (sl_stack_next), so a call's k_cloud also runs the next
+    # call's histogram pass and every call but the first starts with k_decode
+    nxt = stack if a.next_stats else None
+
     def step(o, maps=maps, fast=head_fast):
         eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
-                               xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o, stack_ready=ready)
+                               xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o, stack_ready=ready,
+                               next_stack=nxt)
         return None
 
     # --streams S: core.ReconstructorPool, S contexts (own scratch, own
@@ -476,7 +486,7 @@ def main():
         res = pool.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
                                       xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
                                       wait_inputs=False,  # resident inputs; outputs never read meanwhile
-                                      stack_ready=ready)
+                                      stack_ready=ready, next_stack=nxt)
         return res["stream"]
 
     def run_steps(k):
@@ -664,7 +674,7 @@ def main():
                                    + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
                        "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
                        "parallelism": f"views sharded over {world} GPU(s)", "streams_per_gpu": S,
-                       "stack_ready": bool(a.stack_ready)},
+                       "stack_ready": bool(a.stack_ready), "next_stats": bool(a.next_stats)},
             "timing": {"preroll": pre,
                        "step_us": spread(step_us),
                        "step_us_note": "HIP events at every step boundary, on the step's stream; intervals "
@@ -696,7 +706,9 @@ def main():
                                            + ("HIP events around back-to-back re-runs of the launch "
                                               "(sl_time_kernels)" if rerun_ok
                                               else "HIP events around the kernel inside the steps")}},
-            "path": {"kind": "k_stats + k_decode (mask, point decision) + k_cloud" if decide
+            "path": {"kind": ("k_decode (mask, point decision) + k_cloud (+ the next call's histogram pass: "
+                              "sl_stack_next; the first call alone runs k_stats)" if a.next_stats
+                              else "k_stats + k_decode (mask, point decision) + k_cloud") if decide
                              else "k_decode + k_count + k_cloud",
                      "launch_groups": n_groups,
                      "kernel_avg_ms": {slots[0]: decode_ms / max(nl, 1), slots[1]: count_ms / max(nl, 1),

@@ -143,6 +143,20 @@ int sl_mask_counts_to(sl_ctx* ctx, int64_t* device_counts);
  * Not applied while the call's stream is being captured into a graph. */
 int sl_stack_ready(sl_ctx* ctx, void* event);
 
+/* The call AFTER the coming one (a stream of views): arms the NEXT
+ * sl_decode_triangulate on this context (that call only; consumed even when it
+ * fails) to compute, beside its own triangulation (extra workgroups of its last
+ * k_cloud launch), the adaptive-mask histograms (sl_system.py:526-528) of the
+ * first launch group of `stack` [n_views][...] (view stride stack_view_stride,
+ * 16-byte aligned, the same frame size as the coming call).  The call after it
+ * then starts with its decode -- when it is on this context, reads that same
+ * stack pointer, stride, view count and frame size with the adaptive mask, and
+ * nothing ran on the context in between; otherwise it computes its histograms
+ * itself.  The caller promises that `stack` holds the next call's images, in
+ * place by the time the coming call's work starts on its stream, and unchanged
+ * until the next call.  Results are unchanged.  NULL disarms. */
+int sl_stack_next(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_stride, int n_views);
+
 /* A prepared call: sl_decode_triangulate's arguments (without the stream),
  * checked once and kept, so that a stream of views through the same resident
  * buffers (a ring of stack slots, reused outputs) re-enqueues it with two

@@ -162,7 +162,7 @@ class Reconstructor:
                            maps: bool = False, cloud: bool = True, xyz_dtype=torch.float32,
                            poses: torch.Tensor | None = None, fast_f32: bool = False, stream=None,
                            out: dict | None = None, mask_counts: torch.Tensor | None = None,
-                           stack_ready=None):
+                           stack_ready=None, next_stack: torch.Tensor | None = None):
         """Fused decode (+ triangulation) of a device stack.
 
         ``stack`` uint8 [n_img, H, W] or [V, n_img, H, W] on this device;
@@ -182,7 +182,12 @@ class Reconstructor:
         or once that event has completed, whatever is queued on ``stream``;
         the adaptive mask's histogram pass then starts on the context's side
         stream beside the previous call's triangulation (sl_stack_ready).
-        Results are unchanged.
+        ``next_stack`` (uint8, same frame size, contiguous frames, on this
+        device): the stack of the NEXT call on this reconstructor, already in
+        place by the time this call's work starts on ``stream`` and unchanged
+        until that call; this call's triangulation kernel also computes its
+        adaptive-mask histograms, so the next call starts with its decode
+        (sl_stack_next).  Results are unchanged.
         """
         args, res, keep, (V, H, W, cloud) = self._resolve(stack, n_cols, n_rows, texture, mask_mode, maps, cloud,
                                                          xyz_dtype, poses, fast_f32, out)
@@ -198,9 +203,22 @@ class Reconstructor:
             if stack_ready is not None and stack_ready is not False:
                 ev = None if stack_ready is True else ctypes.c_void_p(stack_ready.cuda_event)
                 _lib.check(self._L.sl_stack_ready(self._ctx, ev), self._ctx, "sl_stack_ready")
+            if next_stack is not None:
+                self._declare_next(next_stack, H, W)
             _lib.check(self._L.sl_decode_triangulate(self._ctx, *args, self._stream(stream)), self._ctx,
                        "sl_decode_triangulate")
         return res
+
+    def _declare_next(self, next_stack: torch.Tensor, H: int, W: int) -> None:
+        """sl_stack_next for ``next_stack`` ([n_img, H, W] or [V, n_img, H, W])."""
+        if next_stack.dtype != torch.uint8 or next_stack.device != self.device:
+            raise ValueError("next_stack must be a uint8 tensor on the reconstructor's device")
+        ns = next_stack if next_stack.dim() == 4 else next_stack.unsqueeze(0)
+        if ns.dim() != 4 or tuple(ns.shape[2:]) != (H, W) or ns.stride(3) != 1 or ns.stride(2) != W \
+                or ns.stride(1) != H * W:
+            raise ValueError(f"next_stack must hold contiguous {W}x{H} frames ([n_img, H, W] or [V, n_img, H, W])")
+        _lib.check(self._L.sl_stack_next(self._ctx, ns.data_ptr(), ns.stride(0), ns.shape[0]), self._ctx,
+                   "sl_stack_next")
 
     def _resolve(self, stack, n_cols, n_rows, texture, mask_mode, maps, cloud, xyz_dtype, poses, fast_f32, out):
         """decode_triangulate's argument checks and output buffers -> (the
@@ -444,12 +462,17 @@ class PreparedCall:
 
     def __init__(self, eng: Reconstructor, handle, res: dict, keep):
         self.eng, self._h, self.res, self._keep = eng, handle, res, keep
+        self._hw = tuple(keep[0].shape[-2:])  # the frame (next_stack must match it)
         self._run = eng._L.sl_call_run
 
-    def run(self, stream=None) -> dict:
+    def run(self, stream=None, next_stack: torch.Tensor | None = None) -> dict:
+        """``next_stack``: as decode_triangulate's (the stack of the next call
+        on this reconstructor; sl_stack_next)."""
         eng = self.eng
         s = (stream if stream is not None else torch.cuda.current_stream(eng.device)).cuda_stream
         with eng._lock:
+            if next_stack is not None:
+                eng._declare_next(next_stack, *self._hw)
             rc = self._run(self._h, s)
         if rc:
             _lib.check(rc, eng._ctx, "sl_call_run")
@@ -520,7 +543,9 @@ class ReconstructorPool:
         arguments; ``stream`` is the lane's own and ``out`` the lane's buffers
         when the pool reuses outputs).  ``wait_inputs=False`` skips the wait
         on the caller's stream and the allocator bookkeeping for inputs the
-        caller knows are ready and kept alive (e.g. resident stacks)."""
+        caller knows are ready and kept alive (e.g. resident stacks).
+        ``next_stack``: the stack of THIS LANE's next call (``lanes`` calls
+        later), as Reconstructor.decode_triangulate's."""
         if "stream" in kw:
             raise ValueError("ReconstructorPool picks the stream (one per lane)")
         with self._lock:
@@ -534,6 +559,7 @@ class ReconstructorPool:
                     t.record_stream(st)  # the caller may free it before the lane has read it
         if not wait_inputs and self._outs[i] is not None and kw.get("out") is None and \
                 kw.get("mask_counts") is None and not kw.get("stack_ready"):
+            nxt = kw.pop("next_stack", None)
             # resident inputs into reused outputs: a prepared call per lane and
             # argument set (sl_call_prepare), re-run with one two-argument call
             tex, pos = kw.get("texture"), kw.get("poses")
@@ -549,7 +575,7 @@ class ReconstructorPool:
                     plan[1].close()
                 plan = self._plans[i] = (pkey, pc)
                 self._keys[i] = None
-            res = dict(plan[1].run(st))
+            res = dict(plan[1].run(st, next_stack=nxt))
             res["stream"] = st
             res["lane"] = i
             return res

@@ -224,6 +224,18 @@ struct Params {
   int sb_shift;
   unsigned long long* lb;  // k_fused: look-back granules, one per workgroup of the launch (zeroed before it)
   int64_t lb_n;            // ... their number (k_stats zeroes them)
+  int cloud_gx;            // k_cloud: workgroups per view that triangulate (the grid's x beyond: pre-stats)
+  // k_cloud's pre-stats workgroups (sl_stack_next): the NEXT call's histogram
+  // pass (k_stats' work) for the views of its first launch group, beside this
+  // call's triangulation; null pre_stack: none
+  const uint8_t* pre_stack;
+  int64_t pre_vs;
+  unsigned* pre_hist;      // [pre_views][kHistView] accumulated (zero before the launch)
+  unsigned* pre_zero;      // the following pre-stats buffer: its first pre_zero_words words zeroed
+  int64_t pre_zero_words;
+  int pre_views;           // views of the next call's first group
+  int pre_bpv;             // workgroups per view (k_stats' grid x)
+  int pre_mix;             // pre-stats workgroups spread among the triangulating ones (else after them)
 };
 
 // ---------------------------------------------------------------- helpers ----
@@ -477,27 +489,22 @@ __global__ __launch_bounds__(256) void k_xy_check(const double* xn, int W, const
 constexpr int kHistRepl = 8;
 constexpr int kHistView = kHistRepl * kSlot;  // u32 per view
 
-// grid (blocks per view, views of the group); 16 pixels per thread per step.
-__global__ __launch_bounds__(kThreads) void k_stats(Params p) {
-  __shared__ unsigned s_hist[256 * kHistStride];
-  __shared__ int s_max[kWaves];
+// One workgroup's share of a view's histogram pass: the 16-pixel groups blk,
+// blk + nblk, ... of the view's white (vb) and black (vb + HW) planes into the
+// LDS replicas, then flushed into replica blk % kHistRepl of the view's global
+// histograms gh (kHistView words).  s_hist: 256 * kHistStride words, s_max:
+// kWaves ints (holds workgroup barriers).
+__device__ __forceinline__ void stats_pass(const uint8_t* vb, int64_t HW, int64_t blk, int64_t nblk, unsigned* gh,
+                                           unsigned* s_hist, int* s_max) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int view = blockIdx.y;
-  const int64_t HW = p.HW;
-  if (blockIdx.x == 0)  // the next launch group's histograms of this slot (its scratch here)
-    for (int i = tid; i < kHistView; i += kThreads) p.hist_zero[static_cast<int64_t>(view) * kHistView + i] = 0u;
-  if (p.lb && blockIdx.x == 0 && view == 0)  // k_fused's look-back granules (it follows this launch)
-    for (int64_t i = tid; i < p.lb_n; i += kThreads) p.lb[i] = 0ull;
   for (int i = tid; i < 256 * kHistStride; i += kThreads) s_hist[i] = 0u;
   __syncthreads();
-  const uint8_t* vb = p.stack + view * p.stack_vs;
   unsigned* hrow = s_hist + (lane & (kHistRep - 1));
   int mx = -1024;
   const int64_t n16 = HW / 16;  // HW % 16 == 0 on this path
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + tid; i < n16;
-       i += static_cast<int64_t>(gridDim.x) * kThreads) {
+  for (int64_t i = blk * kThreads + tid; i < n16; i += nblk * kThreads) {
     const uint4 wq = *reinterpret_cast<const uint4*>(vb + 16 * i);
     const uint4 bq = *reinterpret_cast<const uint4*>(vb + HW + 16 * i);
 #pragma unroll
@@ -511,7 +518,7 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p) {
   for (int d = 32; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d, 64));
   if (lane == 0) s_max[wid] = mx;
   __syncthreads();
-  unsigned* gh = p.hist + static_cast<int64_t>(view) * kHistView + (blockIdx.x % kHistRepl) * kSlot;
+  gh += (blk % kHistRepl) * kSlot;
   unsigned cnt = 0u;
   const unsigned* row = s_hist + tid * kHistStride;
 #pragma unroll
@@ -523,6 +530,20 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p) {
     for (int w = 1; w < kWaves; ++w) m = max(m, s_max[w]);
     if (m > -1024) atomicMax(gh + 256, static_cast<unsigned>(m + 1024));
   }
+}
+
+// grid (blocks per view, views of the group); 16 pixels per thread per step.
+__global__ __launch_bounds__(kThreads) void k_stats(Params p) {
+  __shared__ unsigned s_hist[256 * kHistStride];
+  __shared__ int s_max[kWaves];
+  const int tid = threadIdx.x;
+  const int view = blockIdx.y;
+  if (blockIdx.x == 0)  // the next launch group's histograms of this slot (its scratch here)
+    for (int i = tid; i < kHistView; i += kThreads) p.hist_zero[static_cast<int64_t>(view) * kHistView + i] = 0u;
+  if (p.lb && blockIdx.x == 0 && view == 0)  // k_fused's look-back granules (it follows this launch)
+    for (int64_t i = tid; i < p.lb_n; i += kThreads) p.lb[i] = 0ull;
+  stats_pass(p.stack + view * p.stack_vs, p.HW, blockIdx.x, gridDim.x, p.hist + static_cast<int64_t>(view) * kHistView,
+             s_hist, s_max);
 }
 
 // Thresholds of a view from its kHistRepl histogram replicas (one wave).
@@ -2086,8 +2107,37 @@ __global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : SLGPU_CLOUD_WAVES) voi
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
-  const int civ = blockIdx.x * kWaves + wid;
-  const int64_t b = static_cast<int64_t>(view) * gridDim.x + blockIdx.x;  // block index in the launch
+  // pre-stats (sl_stack_next): S = gridDim.x - cloud_gx workgroups per view
+  // compute the next call's histograms, after the triangulating ones, or
+  // spread evenly among them (pre_mix: x is a pre-stats workgroup where
+  // floor(x S / T) steps)
+  int cx = blockIdx.x;  // triangulating workgroup index in the view
+  int64_t sx = -1;      // pre-stats workgroup index in the view
+  if (static_cast<int>(gridDim.x) > p.cloud_gx) {
+    const int64_t T = gridDim.x, S = T - p.cloud_gx, x = blockIdx.x;
+    if (p.pre_mix) {
+      const int64_t s0 = x * S / T, s1 = (x + 1) * S / T;
+      if (s1 != s0) sx = s0;
+      cx = static_cast<int>(x - s1);
+    } else if (x >= p.cloud_gx) {
+      sx = x - p.cloud_gx;
+    }
+  }
+  const int civ = cx * kWaves + wid;
+  if (sx >= 0) {
+    const int64_t nsx = gridDim.x - p.cloud_gx;
+    const int64_t sblk = static_cast<int64_t>(view) * nsx + sx;
+    const int64_t total = static_cast<int64_t>(p.pre_views) * p.pre_bpv;
+    for (int64_t i = sblk * kThreads + tid; i < p.pre_zero_words; i += static_cast<int64_t>(gridDim.y) * nsx * kThreads)
+      p.pre_zero[i] = 0u;  // the buffer the following pre-stats pass accumulates into
+    if (sblk < total) {
+      const int pv = static_cast<int>(sblk / p.pre_bpv);
+      stats_pass(p.pre_stack + pv * p.pre_vs, p.HW, sblk - static_cast<int64_t>(pv) * p.pre_bpv, p.pre_bpv,
+                 p.pre_hist + static_cast<int64_t>(pv) * kHistView, &s_ent[0][0], reinterpret_cast<int*>(s_wred));
+    }
+    return;
+  }
+  const int64_t b = static_cast<int64_t>(view) * p.cloud_gx + cx;  // block index in the launch
   const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
   // (SLGPU_CLOUD_HOIST: the chunk's own loads before the offset's; measured slower)
   ChunkIn in;
@@ -2300,6 +2350,29 @@ struct sl_ctx {
   bool side_groups = false;       // SLGPU_STATS_SIDE=1: also the later launch groups of every call (A/B;
                                   // off by default: a cross-stream event wait measured 10-20 us of latency,
                                   // more than the k_stats it hides)
+  // Pre-stats (sl_stack_next): a call's last k_cloud also runs the histogram
+  // pass of the NEXT call's first launch group (declared stack), so that call
+  // starts with its k_decode.  Three buffers in rotation: the one the current
+  // call's k_decode reads, the one its k_cloud accumulates into, and the one
+  // that k_cloud zeroes for the following pass (last read a call earlier).
+  unsigned* d_pre[3] = {nullptr, nullptr, nullptr};
+  int64_t cap_pre = 0;                // words of each
+  int64_t pre_dirty[3] = {0, 0, 0};   // leading words that may be non-zero
+  int pre_acc = 0;                    // buffer the next pre-stats pass accumulates into
+  bool decl_next = false;             // sl_stack_next armed for the coming call
+  const uint8_t* decl_stack = nullptr;
+  int64_t decl_vs = 0;
+  int decl_views = 0;
+  bool pre_armed = false;             // a pre-stats pass was queued for the next call
+  int pre_buf = 0;                    // ... into this buffer
+  const uint8_t* pre_stack = nullptr; // ... of this stack, stride, first-group views, frame
+  int64_t pre_vs = 0, pre_hw = 0;
+  int pre_views = 0;
+  bool no_pre = false;                // SLGPU_PRESTATS=0: sl_stack_next ignored (A/B)
+  int pre_mix = 0;                    // SLGPU_PRE_MIX=1: pre-stats workgroups spread among k_cloud's (A/B)
+  int pre_wgs = 0;                    // SLGPU_PRE_WGS=n: pre-stats workgroups in all (A/B; 0: k_stats' grid)
+  bool decode_balance = false;        // SLGPU_DECODE_BALANCE=1: the capped k_decode grid shrunk so that every
+                                      // workgroup decodes the same number of chunk groups (A/B)
   struct {
     bool valid = false;
     bool decide = false;  // fn[1] = k_stats (or null) instead of k_count
@@ -2523,6 +2596,36 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
   if (r) return r;
   r = grow(c, &c->d_stats, &c->cap_stats, p0.n_views);
   if (r) return r;
+  // Pre-stats (sl_stack_next): this call's first group takes the histograms
+  // the previous call's k_cloud computed for it (same stack, stride, views
+  // and frame), and this call's last k_cloud computes those of the call
+  // declared next.  (Not with k_fused, whose look-back granules k_stats zeroes.)
+  const int nv0 = std::min(vpg, p0.n_views);
+  bool pre_use = c->pre_armed && decide && adaptive && !c->fused && p0.stack == c->pre_stack &&
+                 p0.stack_vs == c->pre_vs && nv0 == c->pre_views && p0.HW == c->pre_hw;
+  c->pre_armed = false;
+  const int pre_in = c->pre_buf;
+  const bool pre_run = c->decl_next && !c->no_pre && !c->fused && cloud_mode >= 0 && vec;
+  c->decl_next = false;
+  int pre_nv = 0;
+  int64_t pre_bpv = 0;
+  if (pre_run) {
+    pre_nv = std::min(vpg, c->decl_views);
+    const int64_t per_view = (p0.HW / 16 + kThreads - 1) / kThreads;
+    const int64_t wgs = c->pre_wgs > 0 ? c->pre_wgs : 2 * c->n_cu;
+    pre_bpv = std::max<int64_t>(1, std::min<int64_t>(per_view, (wgs + pre_nv - 1) / pre_nv));
+    const int64_t words = static_cast<int64_t>(pre_nv) * kHistView;
+    if (words > c->cap_pre) {  // (re)allocated zeroed: nothing left to take
+      pre_use = false;
+      for (int b = 0; b < 3; ++b) {
+        int64_t cap = c->cap_pre;
+        r = grow(c, &c->d_pre[b], &cap, words);
+        if (r) return r;
+        if (b == 2) c->cap_pre = cap;
+        c->pre_dirty[b] = 0;
+      }
+    }
+  }
   c->last_views = p0.n_views;
   if (p0.masked)  // the caller's per-view counts, accumulated by the groups' k_decode / k_count
     HIP_TRY(c, hipMemsetAsync(p0.masked, 0, sizeof(unsigned long long) * p0.n_views, s));
@@ -2561,7 +2664,8 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     // histograms it zeroes (the previous group's or call's k_decode) and, for
     // a call's first group, the caller's readiness event (else after
     // everything queued so far: the side path's first use)
-    const bool ahead = side_ok && ((g > 0 && c->side_groups) || (g == 0 && ready));
+    const bool pre_g = pre_use && g == 0;  // histograms computed by the previous call's k_cloud
+    const bool ahead = !pre_g && side_ok && ((g > 0 && c->side_groups) || (g == 0 && ready));
     hipStream_t ss = ahead ? c->side : s;
     if (g == 0 && ready_ev && !ahead) HIP_TRY(c, hipStreamWaitEvent(s, ready_ev, 0));  // the promise, kept on s
     if (ahead) {
@@ -2574,7 +2678,10 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
         HIP_TRY(c, hipStreamWaitEvent(ss, c->hist_ev, 0));
       }
     }
-    if (adaptive) {  // hist_dirty: leading words of a buffer that may be non-zero
+    if (pre_g) {
+      p.hist = c->d_pre[pre_in];
+      p.hist_zero = nullptr;
+    } else if (adaptive) {  // hist_dirty: leading words of a buffer that may be non-zero
       const int a = c->par, b = 1 - c->par;
       const int64_t words = static_cast<int64_t>(nv) * (decide ? kHistView : kSlot);
       if (c->hist_dirty[a] > 0)
@@ -2599,6 +2706,10 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     c->last.valid = true;
     dim3 dgrid = grid;  // k_decode: chunk groups strided over a capped grid
     if (c->decode_wgs > 0) dgrid.x = std::min(grid.x, static_cast<unsigned>(std::max(1, (c->decode_wgs + nv - 1) / nv)));
+    if (c->decode_balance) {  // rounds of the capped grid, and the fewest workgroups that need no more
+      const unsigned rounds = (grid.x + dgrid.x - 1) / dgrid.x;
+      dgrid.x = (grid.x + rounds - 1) / rounds;
+    }
     c->last.grid[0] = dgrid;
     // barrier-free block sums when every k_decode workgroup iterates at most
     // kBsSlots chunk groups (4 chunks of at most 1024 points: 16-bit sums)
@@ -2622,7 +2733,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     }
     if (decide) {
       c->last.fn[1] = nullptr;
-      if (adaptive) {  // k_stats: the thresholds' histograms, before the decode applies them
+      if (adaptive && !pre_g) {  // k_stats: the thresholds' histograms, before the decode applies them
         const int64_t per_view = (p0.HW / 16 + kThreads - 1) / kThreads;
         const dim3 sg(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(per_view, (2 * c->n_cu + nv - 1) / nv))),
                       static_cast<unsigned>(nv));
@@ -2676,12 +2787,40 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     if (gev && !decide) HIP_TRY(c, hipEventRecord(gev[2], s));
     if (cloud_mode >= 0 && !fusedfn) {
       p.mode = cloud_mode;
-      void* args[] = {&p};
+      p.cloud_gx = static_cast<int>(grid.x);
       // at most one chunk per SIMD: all of a chunk's points in one pass
       KernelFn fn = pick_cloud(cloud_mode, vec, p.n_chunks <= 4 * static_cast<int64_t>(c->n_cu));
-      c->last.p[2] = p;
+      c->last.p[2] = p;  // (sl_time_kernels re-runs it without the pre-stats workgroups)
       c->last.fn[2] = reinterpret_cast<const void*>(fn);
-      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), grid, dim3(kThreads), args, 0, s));
+      Params pc = p;
+      dim3 cgrid = grid;
+      const bool pre_now = pre_run && g == n_groups - 1;
+      if (pre_now) {  // + the declared next call's histogram pass, after this group's triangulating workgroups
+        const int acc = c->pre_acc, zb = (acc + 1) % 3;
+        if (c->pre_dirty[acc] > 0)
+          HIP_TRY(c, hipMemsetAsync(c->d_pre[acc], 0, sizeof(unsigned) * c->pre_dirty[acc], s));
+        pc.pre_stack = c->decl_stack;
+        pc.pre_vs = c->decl_vs;
+        pc.pre_hist = c->d_pre[acc];
+        pc.pre_zero = c->d_pre[zb];
+        pc.pre_zero_words = c->pre_dirty[zb];
+        pc.pre_views = pre_nv;
+        pc.pre_bpv = static_cast<int>(pre_bpv);
+        pc.pre_mix = c->pre_mix;
+        const int64_t total = static_cast<int64_t>(pre_nv) * pre_bpv;
+        cgrid.x += static_cast<unsigned>((total + nv - 1) / nv);
+        c->pre_dirty[acc] = static_cast<int64_t>(pre_nv) * kHistView;
+        c->pre_dirty[zb] = 0;
+        c->pre_acc = zb;
+        c->pre_buf = acc;
+        c->pre_stack = c->decl_stack;
+        c->pre_vs = c->decl_vs;
+        c->pre_views = pre_nv;
+        c->pre_hw = p0.HW;
+      }
+      void* args[] = {&pc};
+      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), cgrid, dim3(kThreads), args, 0, s));
+      if (pre_now) c->pre_armed = true;
     }
     if (gev) HIP_TRY(c, hipEventRecord(gev[3], s));
   }
@@ -2856,6 +2995,10 @@ int sl_ctx_create(int device, sl_ctx** out) {
   }
   if (const char* d = getenv("SLGPU_XY_CALC")) c->xy_calc_env = atoi(d) != 0;
   if (const char* d = getenv("SLGPU_FUSED")) c->fused = atoi(d) != 0;
+  if (const char* d = getenv("SLGPU_PRESTATS")) c->no_pre = atoi(d) == 0;
+  if (const char* d = getenv("SLGPU_PRE_MIX")) c->pre_mix = atoi(d);
+  if (const char* d = getenv("SLGPU_PRE_WGS")) c->pre_wgs = std::max(0, atoi(d));
+  if (const char* d = getenv("SLGPU_DECODE_BALANCE")) c->decode_balance = atoi(d) != 0;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
@@ -2885,7 +3028,8 @@ void sl_ctx_destroy(sl_ctx* c) {
                     static_cast<void*>(c->d_hist[1]), static_cast<void*>(c->d_ptnib),
                     static_cast<void*>(c->d_block_sums), static_cast<void*>(c->d_chunk_counts),
                     static_cast<void*>(c->d_super[0]), static_cast<void*>(c->d_super[1]),
-                    static_cast<void*>(c->d_lb)})
+                    static_cast<void*>(c->d_lb), static_cast<void*>(c->d_pre[0]),
+                    static_cast<void*>(c->d_pre[1]), static_cast<void*>(c->d_pre[2])})
     if (ptr) (void)hipFree(ptr);
   delete c;
 }
@@ -3166,6 +3310,20 @@ int sl_stack_ready(sl_ctx* c, void* event) {
   if (!c) return SL_EINVAL;
   c->ready_next = true;
   c->ready_ev_next = static_cast<hipEvent_t>(event);
+  return SL_OK;
+}
+
+int sl_stack_next(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int n_views) {
+  if (!c) return SL_EINVAL;
+  c->decl_next = false;
+  if (!stack) return SL_OK;  // disarm
+  if (n_views < 1) return fail(c, SL_EINVAL, "sl_stack_next: n_views must be >= 1");
+  if (!aligned16(stack) || stack_vs % 16 != 0 || stack_vs < 0)
+    return fail(c, SL_EINVAL, "sl_stack_next: the stack and its view stride must be 16-byte aligned");
+  c->decl_next = true;
+  c->decl_stack = stack;
+  c->decl_vs = stack_vs;
+  c->decl_views = n_views;
   return SL_OK;
 }
 

@@ -1,0 +1,198 @@
+"""sl_stack_next (pre-stats): a call's k_cloud also runs the NEXT call's
+adaptive-mask histogram pass (sl_system.py:526-528), so that call starts with
+its decode.  Bar: every call's maps, mask, thresholds and cloud bit-identical
+to the same call made alone, whatever the chain does (declared stacks taken,
+mismatched declarations ignored, fixed-mask calls in between, multi-group
+calls, the pool's prepared calls, kernel re-runs in between), and the oracle's
+on a sample (GPU only)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import sl_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def _snap(res, eng):
+    cloud = res["cloud"]
+    off = cloud.offsets()
+    out = [cloud.xyz[: off[-1]].cpu().numpy(), cloud.bgr[: off[-1]].cpu().numpy(), np.asarray(off)]
+    if "col_map" in res:
+        out += [res["col_map"].cpu().numpy(), res["row_map"].cpu().numpy(), res["mask"].cpu().numpy()]
+    out.append(np.array(eng.last_thresholds(0), dtype=np.float64))
+    return out
+
+
+def _same(got, ref, what):
+    for k, (a, b) in enumerate(zip(got, ref)):
+        np.testing.assert_array_equal(a, b, err_msg=f"{what}: output {k}")
+
+
+def test_chained_calls_bit_identical():
+    """Five views, each call naming the next one's stack: adaptive calls take
+    the histograms computed by the previous call's k_cloud; a declaration that
+    does not match the next call (another buffer) is ignored; a fixed-mask call
+    in the chain consumes nothing but still queues the pass for its successor;
+    three rounds go through the three-buffer rotation more than once."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 480, 640
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    views = [synth.render_stack(rig, seed=700 + v, view_deg=20.0 * v, device="cuda") for v in range(5)]
+    modes = ["adaptive", "adaptive", "fixed", "adaptive", "adaptive"]
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    ref = []
+    for (st, tx), mm in zip(views, modes):
+        r = eng.decode_triangulate(st, texture=tx, mask_mode=mm, maps=True, cloud=True, xyz_dtype=torch.float32,
+                                   out={})
+        eng.sync()
+        ref.append(_snap(r, eng))
+    decoy = views[0][0].clone()  # same content, another buffer: the declaration must not be taken for it
+    for rnd in range(3):
+        for i, ((st, tx), mm) in enumerate(zip(views, modes)):
+            nxt = views[(i + 1) % len(views)][0]
+            if rnd == 1 and i == 1:
+                nxt = decoy  # call 2 is on views[2]: computes its own (fixed mask anyway)
+            if rnd == 1 and i == 2:
+                nxt = decoy  # call 3 is on views[3], not the decoy: k_stats runs
+            r = eng.decode_triangulate(st, texture=tx, mask_mode=mm, maps=True, cloud=True,
+                                       xyz_dtype=torch.float32, out={}, next_stack=nxt)
+            eng.sync()
+            _same(_snap(r, eng), ref[i], f"round {rnd}, call {i}")
+    st, tx = views[1]
+    col, row, mask, P, C = o.decode_triangulate(list(st.cpu().numpy()), tx.cpu().numpy(), cal)
+    np.testing.assert_array_equal(ref[1][3][0], col)
+    np.testing.assert_array_equal(ref[1][5][0], mask)
+    np.testing.assert_array_equal(ref[1][0], P.astype(np.float32))
+
+
+@pytest.mark.parametrize("env", [{}, {"SLGPU_PRE_MIX": "1"}, {"SLGPU_PRE_WGS": "7"},
+                                 {"SLGPU_PRE_MIX": "1", "SLGPU_PRE_WGS": "600"}])
+def test_chained_calls_without_syncs(env, monkeypatch):
+    """The same chain queued back to back (no host sync between calls, each
+    call into its own outputs): the pass a call's k_cloud runs and the next
+    call's decode are ordered by the stream alone.  Also with the pre-stats
+    workgroups spread among the triangulating ones, and with fewer / more of
+    them than k_stats' grid (A/B switches, read at context creation)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 240, 320
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    views = [synth.render_stack(rig, seed=40 + v, view_deg=33.0 * v, device="cuda") for v in range(4)]
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    ref = []
+    for st, tx in views:
+        r = eng.decode_triangulate(st, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out={})
+        eng.sync()
+        ref.append(_snap(r, eng))
+    order = [0, 1, 2, 3, 3, 2, 1, 0, 0, 1]
+    res = []
+    for k, v in enumerate(order):
+        st, tx = views[v]
+        nxt = views[order[k + 1]][0] if k + 1 < len(order) else None
+        res.append(eng.decode_triangulate(st, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out={},
+                                          next_stack=nxt))
+    eng.sync()
+    for k, (v, r) in enumerate(zip(order, res)):
+        _same(_snap(r, eng)[:-1], ref[v][:-1], f"call {k} (view {v})")
+
+
+def test_chained_multi_group_calls():
+    """Calls of two launch groups (34 1080p views: 32 + 2): the last group's
+    k_cloud computes the histograms of the next call's first group (32 views);
+    that call's second group runs its own k_stats."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W, V = 1080, 1920, 34
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig, with_Nc=False)
+    base = [synth.render_stack(rig, seed=60 + v, view_deg=40.0 * v, device="cuda", include_rows=False)
+            for v in range(3)]
+    n_img = base[0][0].shape[0]
+    A = torch.empty((V, n_img, H, W), dtype=torch.uint8, device="cuda")
+    TA = torch.empty((V, H, W, 3), dtype=torch.uint8, device="cuda")
+    for v in range(V):
+        A[v].copy_(base[v % 3][0])
+        TA[v].copy_(base[v % 3][1])
+    B, TB = A.roll(1, 0).contiguous(), TA.roll(1, 0).contiguous()
+    del base
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    ref = {}
+    for name, (st, tx) in {"A": (A, TA), "B": (B, TB)}.items():
+        r = eng.decode_triangulate(st, texture=tx, cloud=True, xyz_dtype=torch.float32, out={})
+        eng.sync()
+        assert eng.last_launch_info()[1] == 2
+        ref[name] = _snap(r, eng)
+    for k, (name, (st, tx), nxt) in enumerate([("A", (A, TA), B), ("B", (B, TB), A), ("A", (A, TA), None)]):
+        r = eng.decode_triangulate(st, texture=tx, cloud=True, xyz_dtype=torch.float32, out={}, next_stack=nxt)
+        eng.sync()
+        _same(_snap(r, eng)[:-1], ref[name][:-1], f"call {k} ({name})")
+
+
+def test_chain_survives_kernel_reruns():
+    """sl_time_kernels between chained calls (it re-runs the last group's
+    kernels, the pre-stats workgroups left out): the next call still takes
+    intact histograms."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 480, 640
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    st, tx = synth.render_stack(rig, seed=5, view_deg=10.0, device="cuda")
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    r = eng.decode_triangulate(st, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out={})
+    eng.sync()
+    ref = _snap(r, eng)
+    for k in range(3):
+        r = eng.decode_triangulate(st, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out={},
+                                   next_stack=st)
+        eng.sync()
+        _same(_snap(r, eng), ref, f"call {k}")
+        eng.time_kernels(3)
+
+
+def test_pool_prepared_calls_with_next_stack():
+    """ReconstructorPool's resident-input path (prepared calls per lane), each
+    call naming the stack of its lane's next call, the bench's c3 / c4 / c5
+    shape: every call's cloud equal to the plain engine's."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W, V = 240, 320, 3
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    sts = [synth.render_stack(rig, seed=80 + v, view_deg=15.0 * v, device="cuda") for v in range(V)]
+    stack = torch.stack([s for s, _ in sts])
+    tex = torch.stack([t for _, t in sts])
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    r = eng.decode_triangulate(stack, texture=tex, maps=True, cloud=True, xyz_dtype=torch.float32, out={})
+    eng.sync()
+    ref = _snap(r, eng)[:-1]
+    pool = core.ReconstructorPool(torch.device("cuda", 0), lanes=2, reuse_outputs=True)
+    pool.set_calibration(cal, H, W)
+    for k in range(6):
+        res = pool.decode_triangulate(stack, texture=tex, maps=True, cloud=True, xyz_dtype=torch.float32,
+                                      wait_inputs=False, next_stack=stack)
+        pool.sync()
+        _same(_snap(res, pool.engines[res["lane"]])[:-1], ref, f"pool call {k}")
+
+
+def test_next_stack_argument_checks():
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 96, 128
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    st, tx = synth.render_stack(rig, seed=1, device="cuda")
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    with pytest.raises(ValueError):
+        eng.decode_triangulate(st, texture=tx, next_stack=st[:, :, : W // 2])  # another frame size
+    with pytest.raises(ValueError):
+        eng.decode_triangulate(st, texture=tx, next_stack=st.float())
+    with pytest.raises(Exception):  # 16-byte alignment (sl_stack_next)
+        flat = torch.empty(st.numel() + 1, dtype=torch.uint8, device="cuda")
+        eng.decode_triangulate(st, texture=tx, next_stack=flat[1:].view(st.shape))
