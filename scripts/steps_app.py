@@ -1,0 +1,35 @@
+"""The bench's steady state for PMC passes: N chained c2 steps (maps + exact
+cloud, each call naming the next call's stack, sl_stack_next) on one
+synthetic 4K view, nothing else on the GPU after set-up except the torch
+copies of the rendering.  scripts/traffic_from_pmc.py --per-step N then
+divides every step kernel's summed bytes by N (the first call's k_stats,
+which no earlier call computed, is 1/N of a k_stats per step).
+
+    python scripts/steps_app.py [--steps 40] [--no-next-stats]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from structured_light_for_3d_model_replication_amd import core, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--steps", type=int, default=40)
+ap.add_argument("--no-next-stats", dest="next_stats", action="store_false", default=True)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+rig = synth.Rig(H=2160, W=3840)
+cal = synth.make_calibration(rig, with_Nc=False)
+st, tx = synth.render_stack(rig, seed=2000, device=dev)
+eng = core.Reconstructor(dev)
+eng.set_calibration(cal, rig.H, rig.W)
+out = {}
+nxt = st if a.next_stats else None
+for _ in range(a.steps):
+    eng.decode_triangulate(st, 1920, 1080, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out=out,
+                           next_stack=nxt)
+eng.sync()
+print(f"steps {a.steps} points {int(out['view_offsets'][-1].item())}")

@@ -5,7 +5,11 @@ coalesced reads at half, MI355X_MICROARCH.md "HBM") + WRITE_SIZE, both in KB
 (x1024); each kernel launches once per step.
 
     python scripts/traffic_from_pmc.py <fetch_dir> <write_dir> <config> <views> <xyz fast|exact> <decide 0|1> <out.json>
-        [--calib <cal_fetch_dir> <cal_write_dir> <store_calib stdout json>]
+        [--calib <cal_fetch_dir> <cal_write_dir> <store_calib stdout json>] [--per-step N]
+
+--per-step N (a command that runs N steps and nothing else, scripts/steps_app.py):
+every kernel's bytes summed over its launches and divided by N, instead of
+one average launch per kernel per step.
 """
 import csv
 import glob
@@ -17,6 +21,9 @@ import sys
 STEP_KERNELS = ("k_stats", "k_decode", "k_count", "k_cloud")  # (sl_set_calib's k_xy_check is not a step's)
 
 
+PER_STEP = None  # --per-step N
+
+
 def per_kernel(d, counter):
     acc = {}
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
@@ -26,7 +33,7 @@ def per_kernel(d, counter):
             m = re.search(r"(k_\w+<[^>]*>|k_\w+)\(", r["Kernel_Name"])
             if m and m.group(1).split("<")[0] in STEP_KERNELS:
                 acc.setdefault(m.group(1), []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return {k: sum(v) / (PER_STEP or len(v)) for k, v in acc.items()}
 
 
 def calib_factors(fdir, wdir, cal_json):
@@ -61,6 +68,10 @@ if "--calib" in args:
     i = args.index("--calib")
     cal = calib_factors(args[i + 1], args[i + 2], args[i + 3])
     del args[i:i + 4]
+if "--per-step" in args:
+    i = args.index("--per-step")
+    PER_STEP = int(args[i + 1])
+    del args[i:i + 2]
 fetch, write = per_kernel(args[0], "FETCH_SIZE"), per_kernel(args[1], "WRITE_SIZE")
 cfg, views, xyz, decide, out = args[2], int(args[3]), args[4], args[5] == "1", args[6]
 kern = {k: (2 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024 for k in sorted(set(fetch) | set(write))}
@@ -90,7 +101,9 @@ res = {
     "bytes_per_step_raw": sum(kern.values()),
     "kernels": short,
     "calibration": cal,
-    "method": ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over scripts/kbench.py "
+    "per_step": PER_STEP,
+    "method": (("every kernel's bytes summed over the launches of %d chained steps (scripts/steps_app.py) / %d; "
+                % (PER_STEP, PER_STEP) if PER_STEP else "") + "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over scripts/kbench.py "
                "(one output mode: every k_* kernel launch belongs to the step); " +
                ("HBM bytes per launch = reported bytes x the calibration factor of the kernel's access shapes, "
                 "measured on known byte counts by scripts/micro/store_calib in the same call (16-B / 12-B / "
