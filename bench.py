@@ -514,6 +514,7 @@ def main():
             st = one()
             if evs:
                 evs[i + 1].record(st)
+        t_enq = time.perf_counter()
         sync_all()
         # this rank's K steps are complete here; the closing barrier's own
         # latency stays out of the interval (the max over ranks covers skew)
@@ -525,7 +526,10 @@ def main():
             # per-step intervals are those of the sorted completion times
             tc = sorted(evs[0].elapsed_time(evs[i + 1]) for i in range(k))
             us = [1e3 * (b - a_) for a_, b in zip([0.0] + tc[:-1], tc)]
+        host_enq_ms[0] = 1e3 * (t_enq - t0)
         return el, us
+
+    host_enq_ms = [None]
 
     def preroll(ms):
         """Back-to-back steps for ``ms`` of wall time (a sync every 16 steps)."""
@@ -551,6 +555,7 @@ def main():
     try:
         pre = preroll(a.preroll_ms)
         el_rank, _ = timed(a.steps)
+        enq_ms = host_enq_ms[0]
         el_ev, step_us = timed(a.steps, evs)
     finally:
         gc.enable()
@@ -682,6 +687,9 @@ def main():
                                        "different streams), in an identical window right after the timed one "
                                        "(the events add ~5.7 us of idle per step: not in the headline window)",
                        "ms_per_step_with_events": 1e3 * el_ev / a.steps,
+                       "host_enqueue_ms": enq_ms,
+                       "host_enqueue_note": "host time to enqueue the headline window's K steps (of its wall "
+                                            "time): close to the wall time = the host, not the GPU, set the pace",
                        "gc": "collected before the pre-roll, disabled through the windows"},
             "roofline": {"bound": "hbm", "scope": "whole path per step: every kernel of the step",
                          "achieved": path_gbps, "peak": HBM_PEAK_GBS, "unit": "GB/s",
