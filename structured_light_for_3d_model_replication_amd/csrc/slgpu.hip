@@ -236,6 +236,7 @@ struct Params {
   int pre_views;           // views of the next call's first group
   int pre_bpv;             // workgroups per view (k_stats' grid x)
   int pre_mix;             // pre-stats workgroups spread among the triangulating ones (else after them)
+  int decode_gx;           // k_decode: decoding workgroups per view (0: gridDim.x; beyond: pre-stats)
 };
 
 // ---------------------------------------------------------------- helpers ----
@@ -546,6 +547,24 @@ __global__ __launch_bounds__(kThreads) void k_stats(Params p) {
              s_hist, s_max);
 }
 
+// One pre-stats workgroup (sl_stack_next), number sx of the nsx per grid row
+// that a k_cloud or k_decode launch appends: zeroes its share of the buffer
+// the following pass accumulates into, then runs its share of the next call's
+// histogram pass (k_stats' work) into p.pre_hist.
+__device__ __forceinline__ void pre_stats_block(const Params& p, int64_t sx, int64_t nsx, unsigned* s_hist,
+                                                int* s_max) {
+  const int tid = threadIdx.x;
+  const int64_t sblk = static_cast<int64_t>(blockIdx.y) * nsx + sx;
+  const int64_t total = static_cast<int64_t>(p.pre_views) * p.pre_bpv;
+  for (int64_t i = sblk * kThreads + tid; i < p.pre_zero_words; i += static_cast<int64_t>(gridDim.y) * nsx * kThreads)
+    p.pre_zero[i] = 0u;
+  if (sblk < total) {
+    const int pv = static_cast<int>(sblk / p.pre_bpv);
+    stats_pass(p.pre_stack + pv * p.pre_vs, p.HW, sblk - static_cast<int64_t>(pv) * p.pre_bpv, p.pre_bpv,
+               p.pre_hist + static_cast<int64_t>(pv) * kHistView, s_hist, s_max);
+  }
+}
+
 // Thresholds of a view from its kHistRepl histogram replicas (one wave).
 __device__ __forceinline__ Thresholds view_thresholds(const Params& p, int view, int lane) {
   uint4 b4 = make_uint4(0u, 0u, 0u, 0u);
@@ -650,6 +669,15 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
   const int64_t HW = p.HW;
+  // pre-stats workgroups (sl_stack_next, SLGPU_PRE_DECODE=1) after the
+  // decoding ones: the next call's histograms in this launch's tail
+  // (instantiations for calls with a cloud on the decide path only)
+  constexpr bool kPreRole = MODE < 0 || ((MODE & M_DECIDE) && (MODE & M_CODES) && !(MODE & M_FUSED));
+  if (kPreRole && p.decode_gx > 0 && static_cast<int>(blockIdx.x) >= p.decode_gx) {
+    pre_stats_block(p, blockIdx.x - p.decode_gx, gridDim.x - p.decode_gx, s_lds, s_max);
+    return;
+  }
+  const int gx = p.decode_gx > 0 ? p.decode_gx : static_cast<int>(gridDim.x);  // decoding workgroups per view
   if (decide) {
     if (tid < kBsSlots) s_bsum[tid] = 0u;
     if (tid == 0) s_mcount = 0u;  // published by the barrier of iteration 0 (or the table fill's)
@@ -719,7 +747,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
   // workgroup-uniform loop holds no barrier.
   const int ngroups = (p.cpv + kWaves - 1) / kWaves;
   int mx_acc = -1024;
-  for (int cg = blockIdx.x; cg < ngroups; cg += gridDim.x) {
+  for (int cg = blockIdx.x; cg < ngroups; cg += gx) {
   const int civ = cg * kWaves + wid;  // chunk in view
   const bool live = civ < p.cpv;
   const int64_t px0 = static_cast<int64_t>(civ) * kChunk + lane * kPx;
@@ -2125,16 +2153,7 @@ __global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : SLGPU_CLOUD_WAVES) voi
   }
   const int civ = cx * kWaves + wid;
   if (sx >= 0) {
-    const int64_t nsx = gridDim.x - p.cloud_gx;
-    const int64_t sblk = static_cast<int64_t>(view) * nsx + sx;
-    const int64_t total = static_cast<int64_t>(p.pre_views) * p.pre_bpv;
-    for (int64_t i = sblk * kThreads + tid; i < p.pre_zero_words; i += static_cast<int64_t>(gridDim.y) * nsx * kThreads)
-      p.pre_zero[i] = 0u;  // the buffer the following pre-stats pass accumulates into
-    if (sblk < total) {
-      const int pv = static_cast<int>(sblk / p.pre_bpv);
-      stats_pass(p.pre_stack + pv * p.pre_vs, p.HW, sblk - static_cast<int64_t>(pv) * p.pre_bpv, p.pre_bpv,
-                 p.pre_hist + static_cast<int64_t>(pv) * kHistView, &s_ent[0][0], reinterpret_cast<int*>(s_wred));
-    }
+    pre_stats_block(p, sx, gridDim.x - p.cloud_gx, &s_ent[0][0], reinterpret_cast<int*>(s_wred));
     return;
   }
   const int64_t b = static_cast<int64_t>(view) * p.cloud_gx + cx;  // block index in the launch
@@ -2371,6 +2390,7 @@ struct sl_ctx {
   bool no_pre = false;                // SLGPU_PRESTATS=0: sl_stack_next ignored (A/B)
   int pre_mix = 0;                    // SLGPU_PRE_MIX=1: pre-stats workgroups spread among k_cloud's (A/B)
   int pre_wgs = 0;                    // SLGPU_PRE_WGS=n: pre-stats workgroups in all (A/B; 0: 8 per CU)
+  bool pre_decode = false;            // SLGPU_PRE_DECODE=1: pre-stats workgroups in k_decode's tail (A/B)
   bool decode_balance = false;        // SLGPU_DECODE_BALANCE=1: the capped k_decode grid shrunk so that every
                                       // workgroup decodes the same number of chunk groups (A/B)
   struct {
@@ -2606,6 +2626,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
   c->pre_armed = false;
   const int pre_in = c->pre_buf;
   const bool pre_run = c->decl_next && !c->no_pre && !c->fused && cloud_mode >= 0 && vec;
+  const bool pre_dec = pre_run && decide && c->pre_decode;  // ... in the last k_decode instead (A/B)
   c->decl_next = false;
   int pre_nv = 0;
   int64_t pre_bpv = 0;
@@ -2634,6 +2655,33 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
   hipEvent_t* ev = nullptr;
   if (!c->prof_ev.empty() && kProfEv * (c->prof_n + 1) <= static_cast<int>(c->prof_ev.size()))
     ev = &c->prof_ev[kProfEv * c->prof_n++];
+  // The pre-stats workgroups' arguments on launch parameters pc of a grid
+  // with nv rows: the launch grows by as many workgroups per row as they need
+  // (after its own), and the next call is armed for them.
+  auto add_pre = [&](Params& pc, dim3& grid, int nv) -> int {
+    const int acc = c->pre_acc, zb = (acc + 1) % 3;
+    if (c->pre_dirty[acc] > 0)
+      HIP_TRY(c, hipMemsetAsync(c->d_pre[acc], 0, sizeof(unsigned) * c->pre_dirty[acc], s));
+    pc.pre_stack = c->decl_stack;
+    pc.pre_vs = c->decl_vs;
+    pc.pre_hist = c->d_pre[acc];
+    pc.pre_zero = c->d_pre[zb];
+    pc.pre_zero_words = c->pre_dirty[zb];
+    pc.pre_views = pre_nv;
+    pc.pre_bpv = static_cast<int>(pre_bpv);
+    pc.pre_mix = c->pre_mix;
+    const int64_t total = static_cast<int64_t>(pre_nv) * pre_bpv;
+    grid.x += static_cast<unsigned>((total + nv - 1) / nv);
+    c->pre_dirty[acc] = static_cast<int64_t>(pre_nv) * kHistView;
+    c->pre_dirty[zb] = 0;
+    c->pre_acc = zb;
+    c->pre_buf = acc;
+    c->pre_stack = c->decl_stack;
+    c->pre_vs = c->decl_vs;
+    c->pre_views = pre_nv;
+    c->pre_hw = p0.HW;
+    return SL_OK;
+  };
   int g = 0;  // launch group index
   for (int v0 = 0; v0 < p0.n_views; v0 += vpg, ++g) {
     hipEvent_t* gev = (ev && g < kProfGroups) ? ev + 4 * g : nullptr;
@@ -2764,12 +2812,20 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fusedfn), grid, dim3(kThreads), args, 0, s));
     } else {
       p.mode = decode_mode;
-      void* args[] = {&p};
       KernelFn fn = pick_decode(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode, vec);
       c->last.p[0] = p;
       c->last.p[0].masked = nullptr;  // sl_time_kernels' re-runs leave the caller's counts alone
       c->last.fn[0] = reinterpret_cast<const void*>(fn);
-      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dgrid, dim3(kThreads), args, 0, s));
+      Params pd = p;
+      dim3 pgrid = dgrid;
+      if (pre_dec && g == n_groups - 1) {  // + the declared next call's histogram pass, in k_decode's tail
+        pd.decode_gx = static_cast<int>(dgrid.x);
+        r = add_pre(pd, pgrid, nv);
+        if (r) return r;
+      }
+      void* args[] = {&pd};
+      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), pgrid, dim3(kThreads), args, 0, s));
+      if (pre_dec && g == n_groups - 1) c->pre_armed = true;
     }
     if (adaptive && decide && (c->hist_tracked || (side_ok && c->side_groups && g + 1 < n_groups))) {
       HIP_TRY(c, hipEventRecord(c->hist_ev, s));  // the last reader of this group's histograms
@@ -2796,29 +2852,10 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->last.fn[2] = reinterpret_cast<const void*>(fn);
       Params pc = p;
       dim3 cgrid = grid;
-      const bool pre_now = pre_run && g == n_groups - 1;
+      const bool pre_now = pre_run && !pre_dec && g == n_groups - 1;
       if (pre_now) {  // + the declared next call's histogram pass, after this group's triangulating workgroups
-        const int acc = c->pre_acc, zb = (acc + 1) % 3;
-        if (c->pre_dirty[acc] > 0)
-          HIP_TRY(c, hipMemsetAsync(c->d_pre[acc], 0, sizeof(unsigned) * c->pre_dirty[acc], s));
-        pc.pre_stack = c->decl_stack;
-        pc.pre_vs = c->decl_vs;
-        pc.pre_hist = c->d_pre[acc];
-        pc.pre_zero = c->d_pre[zb];
-        pc.pre_zero_words = c->pre_dirty[zb];
-        pc.pre_views = pre_nv;
-        pc.pre_bpv = static_cast<int>(pre_bpv);
-        pc.pre_mix = c->pre_mix;
-        const int64_t total = static_cast<int64_t>(pre_nv) * pre_bpv;
-        cgrid.x += static_cast<unsigned>((total + nv - 1) / nv);
-        c->pre_dirty[acc] = static_cast<int64_t>(pre_nv) * kHistView;
-        c->pre_dirty[zb] = 0;
-        c->pre_acc = zb;
-        c->pre_buf = acc;
-        c->pre_stack = c->decl_stack;
-        c->pre_vs = c->decl_vs;
-        c->pre_views = pre_nv;
-        c->pre_hw = p0.HW;
+        r = add_pre(pc, cgrid, nv);
+        if (r) return r;
       }
       void* args[] = {&pc};
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), cgrid, dim3(kThreads), args, 0, s));
@@ -3000,6 +3037,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
   if (const char* d = getenv("SLGPU_PRESTATS")) c->no_pre = atoi(d) == 0;
   if (const char* d = getenv("SLGPU_PRE_MIX")) c->pre_mix = atoi(d);
   if (const char* d = getenv("SLGPU_PRE_WGS")) c->pre_wgs = std::max(0, atoi(d));
+  if (const char* d = getenv("SLGPU_PRE_DECODE")) c->pre_decode = atoi(d) != 0;
   if (const char* d = getenv("SLGPU_DECODE_BALANCE")) c->decode_balance = atoi(d) != 0;
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;

@@ -69,13 +69,15 @@ def test_chained_calls_bit_identical():
 
 
 @pytest.mark.parametrize("env", [{}, {"SLGPU_PRE_MIX": "1"}, {"SLGPU_PRE_WGS": "7"},
-                                 {"SLGPU_PRE_MIX": "1", "SLGPU_PRE_WGS": "600"}])
+                                 {"SLGPU_PRE_MIX": "1", "SLGPU_PRE_WGS": "600"}, {"SLGPU_PRE_DECODE": "1"},
+                                 {"SLGPU_PRE_DECODE": "1", "SLGPU_PRE_WGS": "5"}])
 def test_chained_calls_without_syncs(env, monkeypatch):
     """The same chain queued back to back (no host sync between calls, each
     call into its own outputs): the pass a call's k_cloud runs and the next
     call's decode are ordered by the stream alone.  Also with the pre-stats
     workgroups spread among the triangulating ones, and with fewer / more of
-    them than k_stats' grid (A/B switches, read at context creation)."""
+    them than k_stats' grid, and with them in k_decode's tail instead (A/B
+    switches, read at context creation)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     from structured_light_for_3d_model_replication_amd import core, synth
