@@ -123,6 +123,11 @@ def parse(argv=None):
                     help="every call names the next call's (resident) stack (sl_stack_next): its triangulation "
                          "kernel also computes the next call's adaptive-mask histograms (default)")
     ap.add_argument("--no-next-stats", dest="next_stats", action="store_false")
+    ap.add_argument("--graph", dest="graph", action="store_true", default=True,
+                    help="one view in flight: the headline window replays a hipGraph of its K steps, captured "
+                         "(untimed) right after the pre-roll -- every kernel of every step runs, the host enqueues "
+                         "nothing inside the window (default; falls back to eager calls if capture fails)")
+    ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r03_traffic_c2.json"),
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
                          "scripts/traffic_from_pmc.py)")
@@ -476,6 +481,11 @@ def main():
         pool.reserve(V, H * W)
         eng, out = pool.engines[0], pool._outs[0]
 
+    # one view in flight: every step on a stream of the bench's own (a graph
+    # capture needs a non-default stream, and calls captured on it follow the
+    # eager ones with no cross-stream hand-off)
+    if pool is None:
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
     cur = torch.cuda.current_stream(dev)
 
     def one():
@@ -531,6 +541,28 @@ def main():
 
     host_enq_ms = [None]
 
+    def timed_graph(k):
+        """The headline window as one hipGraph launch: the K steps are captured
+        first (untimed; the library's calls enqueue into the graph exactly as
+        onto the stream, host-side state advancing as for K calls), then the
+        graph is launched once between barrier + synchronize pairs.  -> seconds."""
+        g = torch.cuda.CUDAGraph()
+        t_c = time.perf_counter()
+        with torch.cuda.graph(g, stream=cur):
+            for _ in range(k):
+                one()
+        cap_ms = 1e3 * (time.perf_counter() - t_c)
+        if distributed:
+            dist.barrier()
+        sync_all()
+        t0 = time.perf_counter()
+        g.replay()
+        t_enq = time.perf_counter()
+        sync_all()
+        el = time.perf_counter() - t0
+        host_enq_ms[0] = 1e3 * (t_enq - t0)
+        return el, g, cap_ms
+
     def preroll(ms):
         """Back-to-back steps for ``ms`` of wall time (a sync every 16 steps)."""
         n, t_pr = 0, time.perf_counter()
@@ -554,7 +586,21 @@ def main():
     gc.disable()
     try:
         pre = preroll(a.preroll_ms)
-        el_rank, _ = timed(a.steps)
+        window = {"mode": "eager: K calls enqueued inside the window"}
+        graph_keep = None
+        if a.graph and pool is None:
+            try:
+                el_rank, graph_keep, cap_ms = timed_graph(a.steps)
+                window = {"mode": "hipGraph: the K steps captured after the pre-roll (untimed), launched once "
+                                  "inside the window; every kernel of every step runs",
+                          "capture_ms": cap_ms}
+            except Exception as e:  # noqa: BLE001 -- capture unsupported here: the eager window instead
+                window = {"mode": "eager (graph capture failed: %s)" % (str(e)[:160],)}
+                torch.cuda.synchronize(dev)
+                eng.drop_next()  # the captured calls' queued pass never ran
+                el_rank, _ = timed(a.steps)
+        else:
+            el_rank, _ = timed(a.steps)
         enq_ms = host_enq_ms[0]
         el_ev, step_us = timed(a.steps, evs)
     finally:
@@ -687,6 +733,7 @@ def main():
                                        "different streams), in an identical window right after the timed one "
                                        "(the events add ~5.7 us of idle per step: not in the headline window)",
                        "ms_per_step_with_events": 1e3 * el_ev / a.steps,
+                       "window": window,
                        "host_enqueue_ms": enq_ms,
                        "host_enqueue_note": "host time to enqueue the headline window's K steps (of its wall "
                                             "time): close to the wall time = the host, not the GPU, set the pace",

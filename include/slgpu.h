@@ -154,7 +154,9 @@ int sl_stack_ready(sl_ctx* ctx, void* event);
  * nothing ran on the context in between; otherwise it computes its histograms
  * itself.  The caller promises that `stack` holds the next call's images, in
  * place by the time the coming call's work starts on its stream, and unchanged
- * until the next call.  Results are unchanged.  NULL disarms. */
+ * until the next call.  Results are unchanged.  NULL disarms, and also drops a
+ * pass an earlier call queued for the next one (that call then computes its
+ * own histograms: e.g. after a failed graph capture of chained calls). */
 int sl_stack_next(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_stride, int n_views);
 
 /* A prepared call: sl_decode_triangulate's arguments (without the stream),

@@ -209,6 +209,12 @@ class Reconstructor:
                        "sl_decode_triangulate")
         return res
 
+    def drop_next(self) -> None:
+        """sl_stack_next(NULL): the next call computes its own histograms (no
+        pass an earlier call queued for it is taken)."""
+        with self._lock:
+            _lib.check(self._L.sl_stack_next(self._ctx, None, 0, 0), self._ctx, "sl_stack_next")
+
     def _declare_next(self, next_stack: torch.Tensor, H: int, W: int) -> None:
         """sl_stack_next for ``next_stack`` ([n_img, H, W] or [V, n_img, H, W])."""
         if next_stack.dtype != torch.uint8 or next_stack.device != self.device:

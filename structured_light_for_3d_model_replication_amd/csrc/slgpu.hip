@@ -3356,7 +3356,10 @@ int sl_stack_ready(sl_ctx* c, void* event) {
 int sl_stack_next(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int n_views) {
   if (!c) return SL_EINVAL;
   c->decl_next = false;
-  if (!stack) return SL_OK;  // disarm
+  if (!stack) {  // disarm, and drop a pass already queued for the next call (it computes its own)
+    c->pre_armed = false;
+    return SL_OK;
+  }
   if (n_views < 1) return fail(c, SL_EINVAL, "sl_stack_next: n_views must be >= 1");
   if (!aligned16(stack) || stack_vs % 16 != 0 || stack_vs < 0)
     return fail(c, SL_EINVAL, "sl_stack_next: the stack and its view stride must be 16-byte aligned");

@@ -198,3 +198,49 @@ def test_next_stack_argument_checks():
     with pytest.raises(Exception):  # 16-byte alignment (sl_stack_next)
         flat = torch.empty(st.numel() + 1, dtype=torch.uint8, device="cuda")
         eng.decode_triangulate(st, texture=tx, next_stack=flat[1:].view(st.shape))
+
+
+def test_graph_captured_chain():
+    """bench.py's headline window: K chained calls (next_stack) captured into
+    a hipGraph on a side stream after eager calls on it, replayed once, then
+    eager calls again -- every call's outputs equal to the plain call's; and
+    a dropped chain (drop_next) computes its own histograms."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 480, 640
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    st, tx = synth.render_stack(rig, seed=11, view_deg=5.0, device="cuda")
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    ref = _snap(eng.decode_triangulate(st, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out={}),
+                eng)
+    s = torch.cuda.Stream()
+    outs = [{} for _ in range(5)]
+    with torch.cuda.stream(s):
+        for o in outs:  # eager calls (allocate the outputs), chained
+            eng.decode_triangulate(st, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out=o,
+                                   next_stack=st)
+    torch.cuda.synchronize()
+    for o in outs:
+        for v in o.values():
+            v.zero_()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    res = []
+    with torch.cuda.graph(g, stream=s):
+        for o in outs:
+            res.append(eng.decode_triangulate(st, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32,
+                                              out=o, next_stack=st))
+    with torch.cuda.stream(s):
+        g.replay()
+    torch.cuda.synchronize()
+    for k, r in enumerate(res):
+        _same(_snap(r, eng)[:-1], ref[:-1], f"graph call {k}")
+    with torch.cuda.stream(s):  # eager again after the replay, then a dropped chain
+        r = eng.decode_triangulate(st, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out={},
+                                   next_stack=st)
+        eng.drop_next()
+        r2 = eng.decode_triangulate(st, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out={})
+    torch.cuda.synchronize()
+    _same(_snap(r, eng)[:-1], ref[:-1], "eager after replay")
+    _same(_snap(r2, eng)[:-1], ref[:-1], "after drop_next")
