@@ -548,7 +548,8 @@ def main():
         graph is launched once between barrier + synchronize pairs.  -> seconds."""
         g = torch.cuda.CUDAGraph()
         t_c = time.perf_counter()
-        with torch.cuda.graph(g, stream=cur):
+        # thread-local capture: other threads' calls (RCCL's proxy threads) are not disturbed
+        with torch.cuda.graph(g, stream=cur, capture_error_mode="thread_local"):
             for _ in range(k):
                 one()
         cap_ms = 1e3 * (time.perf_counter() - t_c)
