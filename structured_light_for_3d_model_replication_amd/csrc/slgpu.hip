@@ -181,6 +181,7 @@ struct Params {
   int Wp;
   const double4* planes;   // (n0, n1, n2, num = n.Oc + d) per projector column
   const float4* planes32;  // f32 (n0, n1, n2, -) for the point/no-point pre-decision
+  const float* planes12;   // the same (n0, n1, n2) packed, 12 B per column (+ 1 KB of slack)
   const double* xn;        // (u - cx) / fx
   const double* yn;        // (v - cy) / fy
   const float* xn32;
@@ -608,10 +609,19 @@ constexpr bool kDecYnLds = SLGPU_DEC_YN_LDS != 0;  // yn in LDS (else one early 
 #define SLGPU_DEC_GLDS 1
 #endif
 constexpr bool kDecGlds = SLGPU_DEC_GLDS != 0;  // decision tables by LDS-DMA, overlapping the first stack loads
-constexpr int kDecPl = 2048, kDecX = 4096, kDecY = 4096;
+#ifndef SLGPU_DEC_PL3
+#define SLGPU_DEC_PL3 0
+#endif
+// (measurement build, SLGPU_DEC_PL3=1: the decision's plane table as packed
+// (n0, n1, n2) floats, 12 B per projector column, Wp <= 1920: 38.4 KB of
+// tables, so that 4 workgroups fit a CU's LDS -- with -DSLGPU_DECODE_WAVES=4
+// -DSLGPU_DECODE_PER_CU=4)
+constexpr bool kDecPl3 = SLGPU_DEC_PL3 != 0;
+constexpr int kDecPl = kDecPl3 ? 1920 : 2048, kDecX = 4096, kDecY = 4096;
+constexpr int kDecPlWords = kDecPl3 ? (kDecPl * 12 + 1023) / 1024 * 256 : kDecPl * 4;  // LDS words of the plane table
 constexpr int kBsSlots = 64;
 constexpr int kSuperCap = 4096;  // super-block sums per launch group (>= sqrt of its blocks)  // k_decode M_DECIDE: chunk-group iterations per workgroup with a barrier-free block sum
-constexpr int kDecodeLds = (kDecPl * 4 + kDecX + (kDecYnLds ? kDecY : 0)) * 4;  // bytes: > the histogram replicas
+constexpr int kDecodeLds = (kDecPlWords + kDecX + (kDecYnLds ? kDecY : 0)) * 4;  // bytes: > the histogram replicas
 static_assert(kDecodeLds >= 256 * kHistStride * 4, "the decode LDS holds the histogram replicas too");
 
 // ================================================================ k_decode ====
@@ -661,7 +671,8 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
   __shared__ unsigned s_mcount;          // M_DECIDE with p.masked: the workgroup's masked pixels
   unsigned* s_hist = s_lds;
   float4* s_pl = reinterpret_cast<float4*>(s_lds);
-  float* s_xn = reinterpret_cast<float*>(s_lds) + 4 * kDecPl;
+  const float* s_pl3 = reinterpret_cast<const float*>(s_lds);
+  float* s_xn = reinterpret_cast<float*>(s_lds) + kDecPlWords;
   float* s_yn = s_xn + kDecX;
   const bool decide = (mode & M_DECIDE) != 0;
   const int tid = threadIdx.x;
@@ -711,12 +722,27 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
       // (iteration 0) publishes them.  Lanes past the end repeat the last
       // entry into slack LDS (kDecPl, kDecX are multiples of 64 entries).
       typedef __attribute__((address_space(3))) void* lds_ptr_t;
-      for (int i = wid; i * 64 < wp_t; i += kWaves)
-        __builtin_amdgcn_global_load_lds(p.planes32 + min(i * 64 + lane, wp_t - 1), (lds_ptr_t)(s_pl + i * 64), 16, 0, 0);
+      if (kDecPl3) {  // the packed 12-B table as bytes, 1 KB per wave instruction (slack: kDecPlWords)
+        const uint8_t* src = reinterpret_cast<const uint8_t*>(p.planes12);
+        for (int i = wid; i * 1024 < wp_t * 12; i += kWaves)
+          __builtin_amdgcn_global_load_lds(src + 16 * (i * 64 + lane), (lds_ptr_t)(s_lds + i * 256), 16, 0, 0);
+      } else {
+        for (int i = wid; i * 64 < wp_t; i += kWaves)
+          __builtin_amdgcn_global_load_lds(p.planes32 + min(i * 64 + lane, wp_t - 1), (lds_ptr_t)(s_pl + i * 64), 16, 0, 0);
+      }
       for (int i = wid; i * 256 < w_t; i += kWaves)
         __builtin_amdgcn_global_load_lds(p.xn32 + min(i * 256 + 4 * lane, w_t - 4), (lds_ptr_t)(s_xn + i * 256), 16, 0, 0);
     } else if (tables) {
-      for (int i = tid; i < wp_t; i += kThreads) s_pl[i] = p.planes32[i];
+      for (int i = tid; i < wp_t; i += kThreads) {
+        if (kDecPl3) {
+          float* d = reinterpret_cast<float*>(s_lds) + 3 * i;
+          d[0] = p.planes12[3 * i];
+          d[1] = p.planes12[3 * i + 1];
+          d[2] = p.planes12[3 * i + 2];
+        } else {
+          s_pl[i] = p.planes32[i];
+        }
+      }
       for (int i = tid; i < w_t; i += kThreads) s_xn[i] = p.xn32[i];
     }
     if (tables && kDecYnLds)
@@ -931,7 +957,10 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
         const int v = px0i / p.W, u0 = px0i - v * p.W;  // the lane's 16 pixels share row v (W % 16 == 0)
         float4 pf[kPx];
 #pragma unroll
-        for (int k = 0; k < kPx; ++k) pf[k] = s_pl[min(col[k], static_cast<uint32_t>(p.Wp - 1))];
+        for (int k = 0; k < kPx; ++k) {
+          const uint32_t ck = min(col[k], static_cast<uint32_t>(p.Wp - 1));
+          pf[k] = kDecPl3 ? make_float4(s_pl3[3 * ck], s_pl3[3 * ck + 1], s_pl3[3 * ck + 2], 0.0f) : s_pl[ck];
+        }
         float xs[kPx];
 #pragma unroll
         for (int q4 = 0; q4 < 4; ++q4) {
@@ -2297,7 +2326,8 @@ struct sl_ctx {
   double* d_planes = nullptr;  // [Wp] (n0, n1, n2, n.Oc + d)
   double* d_xn = nullptr;
   double* d_yn = nullptr;
-  float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H]
+  float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H] | planes12 [Wp][3]
+  size_t off12 = 0;        // floats before planes12
   float fast_thr = 0.0f;   // k_count's sufficient |n.r| threshold (Params::fast_thr)
   bool xy_safe = false;     // every xn / yn table entry is div_safe (Params::xy_safe)
   bool xy_calc = false;     // xy_of reproduces every xn / yn entry (k_xy_check; SLGPU_XY_CALC=0: gathers, A/B)
@@ -3137,7 +3167,12 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
   HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_yn), sizeof(double) * H));
   HIP_TRY(c, hipMemcpy(c->d_yn, yn.data(), sizeof(double) * H, hipMemcpyHostToDevice));
   {
-    std::vector<float> f(4 * static_cast<size_t>(Wp) + W + H);
+    // planes32 [Wp][4] | xn32 [W] | yn32 [H] | pad to 16 B | planes12 [Wp][3] | 1 KB + 16 B of slack
+    const size_t off12 = (4 * static_cast<size_t>(Wp) + W + H + 3) / 4 * 4;
+    std::vector<float> f(off12 + 3 * static_cast<size_t>(Wp) + 260, 0.0f);
+    for (int i = 0; i < Wp; ++i)
+      for (int k = 0; k < 3; ++k) f[off12 + 3 * i + k] = static_cast<float>(pl[4 * i + k]);
+    c->off12 = off12;
     for (int i = 0; i < 4 * Wp; ++i) f[i] = static_cast<float>(pl[i]);  // w: f32 of n.Oc + d
     for (int u = 0; u < W; ++u) f[4 * Wp + u] = static_cast<float>(xn[u]);
     for (int v = 0; v < H; ++v) f[4 * Wp + W + v] = static_cast<float>(yn[v]);
@@ -3251,6 +3286,7 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.planes32 = reinterpret_cast<const float4*>(c->d_f32);
   p.xn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp : nullptr;
   p.yn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp + c->W : nullptr;
+  p.planes12 = c->d_f32 ? c->d_f32 + c->off12 : nullptr;
   p.fast_thr = c->fast_thr;
   p.xy_safe = c->xy_safe ? 1 : 0;
   p.xy_calc = c->xy_calc ? 1 : 0;
