@@ -62,7 +62,7 @@ CONFIGS = {
     # 360-view scan over 8 GPUs (24.8 / 17.2 GB of stacks resident in HBM);
     # c3: the 36-view turntable scan (strong scaling shards it).
     "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0,
-               streams=6),
+               streams=3),  # with next-stats (2 launches per call): 3 lanes best
     "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0),
     "c3": dict(H=1080, W=1920, Wp=1920, Hp=1080, rows=True, views=36, maps=False, pose=False, deg=10.0,
                streams=2),

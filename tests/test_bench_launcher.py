@@ -60,7 +60,7 @@ def test_streams_defaults_per_config():
     import bench
     assert bench.parse([]).streams is None
     assert bench.parse(["--streams", "3"]).streams == 3
-    assert bench.CONFIGS["c1"]["streams"] == 6 and bench.CONFIGS["c5"]["streams"] == 2
+    assert bench.CONFIGS["c1"]["streams"] == 3 and bench.CONFIGS["c5"]["streams"] == 2
     assert bench.CONFIGS["c3"]["streams"] == 2 and bench.CONFIGS["c4"]["streams"] == 2  # measured, DESIGN 5.2
     assert "streams" not in bench.CONFIGS["c2"]
 
