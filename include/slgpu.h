@@ -139,8 +139,10 @@ int sl_mask_counts_to(sl_ctx* ctx, int64_t* device_counts);
  * context's side stream as soon as that holds and the previous call's decode
  * has read its own histograms -- beside the previous call's triangulation --
  * instead of behind everything queued on the call's stream.  Results are
- * unchanged.  (The later launch groups of one large call always do this.)
- * Not applied while the call's stream is being captured into a graph. */
+ * unchanged.  (The later launch groups of one large call need no such
+ * promise: each takes its histograms from a pass the previous group's k_cloud
+ * ran -- pre-stats within the call.)  Not applied while the call's stream is
+ * being captured into a graph. */
 int sl_stack_ready(sl_ctx* ctx, void* event);
 
 /* The call AFTER the coming one (a stream of views): arms the NEXT
@@ -156,7 +158,12 @@ int sl_stack_ready(sl_ctx* ctx, void* event);
  * place by the time the coming call's work starts on its stream, and unchanged
  * until the next call.  Results are unchanged.  NULL disarms, and also drops a
  * pass an earlier call queued for the next one (that call then computes its
- * own histograms: e.g. after a failed graph capture of chained calls). */
+ * own histograms: e.g. after a failed graph capture of chained calls).  A
+ * queued pass is taken or dropped by the very next call on the context, even
+ * one that fails its argument checks (never by a later one).
+ * Within one call of several launch groups (more than 65536 chunks of 1024
+ * pixels) the same happens without any declaration: group g's k_cloud computes
+ * group g + 1's histograms, so only the first group can need a k_stats launch. */
 int sl_stack_next(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_stride, int n_views);
 
 /* A prepared call: sl_decode_triangulate's arguments (without the stream),

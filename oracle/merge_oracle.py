@@ -405,8 +405,8 @@ def estimate_normals(points, radius, max_nn=30):
 #     triangle, row-major), JTr, sum d2, count folded left to right over
 #     64-source-point blocks, then the blocks left to right (Open3D: an
 #     OpenMP reduction, order unspecified);
-#   - 6x6 Cholesky (Open3D: Eigen LDLT), identity update when not positive
-#     definite; x = (alpha, beta, gamma, tx, ty, tz) -> [Rz Ry Rx | t]
+#   - 6x6 pivoted LDLT as Eigen's (Open3D: A.ldlt().solve(b)), zero pivots
+#     -> zero components; x = (alpha, beta, gamma, tx, ty, tz) -> [Rz Ry Rx | t]
 #     (TransformVector6dToMatrix4d), products ((a0 b0 + a1 b1) + a2 b2)
 #     [+ a3 b3];
 #   - transformation = update @ transformation; the source is moved by the
@@ -494,41 +494,73 @@ def mat4(a, b):
 
 
 def icp_update(sums):
-    """JTJ x = -JTr by Cholesky -> the 4x4 update (identity if not SPD)."""
+    """JTJ x = -JTr -> the 4x4 update, as Open3D's SolveLinearSystemPSD
+    (x = A.ldlt().solve(b), no PSD checks): Eigen's LDLT -- left-looking,
+    diagonal pivoting on the largest |a_ii| not yet factored (first on ties),
+    zero pivots left unscaled, and D's pseudo-inverse in the solve (components
+    with |d_i| <= DBL_MIN are 0).  Sums of products left to right (Eigen's
+    vectorised order may differ in the last bits).  Identity only when the
+    solution is not finite."""
     import math
-    A = [[0.0] * 6 for _ in range(6)]
+    import sys
+    M = [[0.0] * 6 for _ in range(6)]
     k = 0
     for a in range(6):
         for c in range(a, 6):
-            A[a][c] = A[c][a] = sums[k]
+            M[a][c] = M[c][a] = sums[k]
             k += 1
-    bb = [-sums[21 + a] for a in range(6)]
+    b = [-sums[21 + a] for a in range(6)]
     ident = [[1.0 if i == j else 0.0 for j in range(4)] for i in range(4)]
-    L = [[0.0] * 6 for _ in range(6)]
+    tr = [0] * 6
+    zero_all = False
     for j in range(6):
-        d = A[j][j]
-        for q in range(j):
-            d = d - L[j][q] * L[j][q]
-        if not (d > 0.0) or not math.isfinite(d):
-            return ident
-        L[j][j] = math.sqrt(d)
+        p = j
         for i in range(j + 1, 6):
-            v = A[i][j]
+            if abs(M[i][i]) > abs(M[p][p]):
+                p = i
+        tr[j] = p
+        if p != j:
+            M[j], M[p] = M[p], M[j]
+            for row in M:
+                row[j], row[p] = row[p], row[j]
+        if j > 0:
+            tmp = [M[q][q] * M[j][q] for q in range(j)]
+            d = 0.0
             for q in range(j):
-                v = v - L[i][q] * L[j][q]
-            L[i][j] = v / L[j][j]
-    y = [0.0] * 6
-    for i in range(6):
-        v = bb[i]
-        for q in range(i):
-            v = v - L[i][q] * y[q]
-        y[i] = v / L[i][i]
-    x = [0.0] * 6
-    for i in range(5, -1, -1):
-        v = y[i]
-        for q in range(i + 1, 6):
-            v = v - L[q][i] * x[q]
-        x[i] = v / L[i][i]
+                d = d + M[j][q] * tmp[q]
+            M[j][j] = M[j][j] - d
+            for i in range(j + 1, 6):
+                v = 0.0
+                for q in range(j):
+                    v = v + M[i][q] * tmp[q]
+                M[i][j] = M[i][j] - v
+        piv = M[j][j]
+        if j == 0 and not (abs(piv) > 0.0):
+            zero_all = True
+            break
+        if abs(piv) > 0.0:
+            for i in range(j + 1, 6):
+                M[i][j] = M[i][j] / piv
+    if zero_all:
+        x = [0.0] * 6
+    else:
+        for j in range(6):
+            b[j], b[tr[j]] = b[tr[j]], b[j]
+        for i in range(6):
+            v = 0.0
+            for q in range(i):
+                v = v + M[i][q] * b[q]
+            b[i] = b[i] - v
+        for i in range(6):
+            b[i] = b[i] / M[i][i] if abs(M[i][i]) > sys.float_info.min else 0.0
+        for i in range(5, -1, -1):
+            v = 0.0
+            for q in range(i + 1, 6):
+                v = v + M[q][i] * b[q]
+            b[i] = b[i] - v
+        for j in range(5, -1, -1):
+            b[j], b[tr[j]] = b[tr[j]], b[j]
+        x = b
     if not all(math.isfinite(v) for v in x):
         return ident
     ca, sa, cb, sb = math.cos(x[0]), math.sin(x[0]), math.cos(x[1]), math.sin(x[1])

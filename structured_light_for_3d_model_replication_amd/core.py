@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import hashlib
 import threading
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -112,8 +113,11 @@ class Reconstructor:
         self._lock = threading.RLock()
         self._calib_key = None
         self._H = self._W = None
+        self._prepared = weakref.WeakSet()  # live PreparedCalls (they hold the context pointer)
 
     def close(self):
+        for pc in list(getattr(self, "_prepared", ())):
+            pc.close()  # before the context they point into
         if getattr(self, "_ctx", None) is not None and self._ctx.value:
             self._L.sl_ctx_destroy(self._ctx)
             self._ctx = ctypes.c_void_p()
@@ -194,20 +198,35 @@ class Reconstructor:
         if mask_counts is not None and (mask_counts.dtype != torch.int64 or mask_counts.device != self.device
                                         or mask_counts.numel() < V or not mask_counts.is_contiguous()):
             raise ValueError(f"mask_counts must be a contiguous int64 tensor of >= {V} entries on {self.device}")
+        nxt = None if next_stack is None else self._next_args(next_stack, H, W)  # every check before any arm
         with self._lock:
             if cloud and (self._H, self._W) != (H, W):
                 raise ValueError(f"calibration is for {self._W}x{self._H}, stack is {W}x{H}")
-            if mask_counts is not None:
-                _lib.check(self._L.sl_mask_counts_to(self._ctx, mask_counts.data_ptr()), self._ctx,
-                           "sl_mask_counts_to")
-            if stack_ready is not None and stack_ready is not False:
-                ev = None if stack_ready is True else ctypes.c_void_p(stack_ready.cuda_event)
-                _lib.check(self._L.sl_stack_ready(self._ctx, ev), self._ctx, "sl_stack_ready")
-            if next_stack is not None:
-                self._declare_next(next_stack, H, W)
+            # the one-call arms of the context, then the call, which consumes
+            # them whatever its outcome; an arm that fails disarms the others
+            try:
+                if nxt is not None:
+                    _lib.check(self._L.sl_stack_next(self._ctx, *nxt), self._ctx, "sl_stack_next")
+                if mask_counts is not None:
+                    _lib.check(self._L.sl_mask_counts_to(self._ctx, mask_counts.data_ptr()), self._ctx,
+                               "sl_mask_counts_to")
+                if stack_ready is not None and stack_ready is not False:
+                    ev = None if stack_ready is True else ctypes.c_void_p(stack_ready.cuda_event)
+                    _lib.check(self._L.sl_stack_ready(self._ctx, ev), self._ctx, "sl_stack_ready")
+            except Exception:
+                self._disarm()
+                raise
             _lib.check(self._L.sl_decode_triangulate(self._ctx, *args, self._stream(stream)), self._ctx,
                        "sl_decode_triangulate")
         return res
+
+    def _disarm(self) -> None:
+        """Clear the one-call arms of the context after a failed arming
+        sequence: no counts pointer, no declared next stack and no queued
+        pre-stats pass (sl_stack_next(NULL)).  (sl_stack_ready is armed last
+        and cannot fail, so it is never left armed by a failure.)"""
+        self._L.sl_mask_counts_to(self._ctx, None)
+        self._L.sl_stack_next(self._ctx, None, 0, 0)
 
     def drop_next(self) -> None:
         """sl_stack_next(NULL): the next call computes its own histograms (no
@@ -215,16 +234,23 @@ class Reconstructor:
         with self._lock:
             _lib.check(self._L.sl_stack_next(self._ctx, None, 0, 0), self._ctx, "sl_stack_next")
 
-    def _declare_next(self, next_stack: torch.Tensor, H: int, W: int) -> None:
-        """sl_stack_next for ``next_stack`` ([n_img, H, W] or [V, n_img, H, W])."""
+    def _next_args(self, next_stack: torch.Tensor, H: int, W: int):
+        """sl_stack_next's arguments for ``next_stack`` ([n_img, H, W] or
+        [V, n_img, H, W]), every check sl_stack_next makes done here first."""
         if next_stack.dtype != torch.uint8 or next_stack.device != self.device:
             raise ValueError("next_stack must be a uint8 tensor on the reconstructor's device")
         ns = next_stack if next_stack.dim() == 4 else next_stack.unsqueeze(0)
         if ns.dim() != 4 or tuple(ns.shape[2:]) != (H, W) or ns.stride(3) != 1 or ns.stride(2) != W \
                 or ns.stride(1) != H * W:
             raise ValueError(f"next_stack must hold contiguous {W}x{H} frames ([n_img, H, W] or [V, n_img, H, W])")
-        _lib.check(self._L.sl_stack_next(self._ctx, ns.data_ptr(), ns.stride(0), ns.shape[0]), self._ctx,
-                   "sl_stack_next")
+        if ns.data_ptr() % 16 or ns.stride(0) % 16 or ns.stride(0) < 0:
+            raise ValueError("sl_stack_next: the stack and its view stride must be 16-byte aligned")
+        return ns.data_ptr(), ns.stride(0), ns.shape[0]
+
+    def _declare_next(self, next_stack: torch.Tensor, H: int, W: int) -> None:
+        """sl_stack_next for ``next_stack`` ([n_img, H, W] or [V, n_img, H, W])."""
+        args = self._next_args(next_stack, H, W)
+        _lib.check(self._L.sl_stack_next(self._ctx, *args), self._ctx, "sl_stack_next")
 
     def _resolve(self, stack, n_cols, n_rows, texture, mask_mode, maps, cloud, xyz_dtype, poses, fast_f32, out):
         """decode_triangulate's argument checks and output buffers -> (the
@@ -296,9 +322,13 @@ class Reconstructor:
         with self._lock:
             if cloud and (self._H, self._W) != (H, W):
                 raise ValueError(f"calibration is for {self._W}x{self._H}, stack is {W}x{H}")
+            if not self._ctx.value:
+                raise RuntimeError("Reconstructor is closed")
             h = ctypes.c_void_p()
             _lib.check(self._L.sl_call_prepare(self._ctx, *args, ctypes.byref(h)), self._ctx, "sl_call_prepare")
-        return PreparedCall(self, h, res, keep)
+            pc = PreparedCall(self, h, res, keep)
+            self._prepared.add(pc)
+        return pc
 
     def triangulate_maps(self, col_map: torch.Tensor, mask: torch.Tensor, texture: torch.Tensor, *,
                          xyz_dtype=torch.float64, poses=None, fast_f32: bool = False, stream=None) -> Cloud:
@@ -476,9 +506,12 @@ class PreparedCall:
         on this reconstructor; sl_stack_next)."""
         eng = self.eng
         s = (stream if stream is not None else torch.cuda.current_stream(eng.device)).cuda_stream
+        nxt = None if next_stack is None else eng._next_args(next_stack, *self._hw)
         with eng._lock:
-            if next_stack is not None:
-                eng._declare_next(next_stack, *self._hw)
+            if not (self._h is not None and self._h.value and eng._ctx.value):
+                raise RuntimeError("PreparedCall is closed (or its Reconstructor is)")
+            if nxt is not None:
+                _lib.check(eng._L.sl_stack_next(eng._ctx, *nxt), eng._ctx, "sl_stack_next")
             rc = self._run(self._h, s)
         if rc:
             _lib.check(rc, eng._ctx, "sl_call_run")

@@ -2153,6 +2153,8 @@ constexpr int kExactPipe = SLGPU_EXACT_PIPE;  // points per lane per pass of the
 #define SLGPU_VERIFY_PIPE 2
 #endif
 constexpr int kVerifyPipe = SLGPU_VERIFY_PIPE;  // ... of the verified-route k_cloud<M_VERIFY | M_TEX>
+static_assert(kWaves * kChunk >= 256 * kHistStride,
+              "k_cloud's pre-stats workgroups keep their LDS histogram replicas in s_ent (SLGPU_HIST_REP <= 14)");
 template <int MODE, int VEC, int PIPE = kPipe>
 __global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : SLGPU_CLOUD_WAVES) void k_cloud(Params p) {
   __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
@@ -2417,7 +2419,8 @@ struct sl_ctx {
   const uint8_t* pre_stack = nullptr; // ... of this stack, stride, first-group views, frame
   int64_t pre_vs = 0, pre_hw = 0;
   int pre_views = 0;
-  bool no_pre = false;                // SLGPU_PRESTATS=0: sl_stack_next ignored (A/B)
+  bool no_pre = false;                // SLGPU_PRESTATS=0: sl_stack_next ignored, no pre-stats at all (A/B)
+  bool no_pre_groups = false;         // SLGPU_PRE_GROUPS=0: no pre-stats between a call's launch groups (A/B)
   int pre_mix = 0;                    // SLGPU_PRE_MIX=1: pre-stats workgroups spread among k_cloud's (A/B)
   int pre_wgs = 0;                    // SLGPU_PRE_WGS=n: pre-stats workgroups in all (A/B; 0: 8 per CU)
   bool pre_decode = false;            // SLGPU_PRE_DECODE=1: pre-stats workgroups in k_decode's tail (A/B)
@@ -2620,11 +2623,29 @@ int ensure_side(sl_ctx* c) {
   return SL_OK;
 }
 
+// The one-call arms of a context (sl_stack_next's declaration, the pre-stats
+// pass an earlier call queued): taken -- and cleared on the context -- at the
+// entry of every call, so that a call that fails before its launch consumes
+// them all the same (a later call on a refilled buffer must never take a
+// histogram of its old contents).
+struct PreArms {
+  bool armed = false;  // the previous call's k_cloud computed histograms for this call (c->pre_*)
+  bool decl = false;   // this call names the next call's stack (c->decl_*)
+};
+PreArms take_arms(sl_ctx* c) {
+  PreArms a;
+  a.armed = c->pre_armed;
+  a.decl = c->decl_next;
+  c->pre_armed = false;
+  c->decl_next = false;
+  return a;
+}
+
 // ready: the caller declared the stack ready (sl_stack_ready; ready_ev, if
 // non-null, completes when it is): the first launch group's k_stats may run on
 // the side stream too.
 int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mode, int cloud_mode,
-           hipStream_t s, bool ready = false, hipEvent_t ready_ev = nullptr) {
+           hipStream_t s, PreArms arms, bool ready = false, hipEvent_t ready_ev = nullptr) {
   const bool decide = (decode_mode & M_DECIDE) != 0;
   const int64_t cpv = p0.cpv;
   const int vpg = static_cast<int>(std::max<int64_t>(1, kMaxChunks / cpv));  // views per group
@@ -2651,23 +2672,28 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
   // and frame), and this call's last k_cloud computes those of the call
   // declared next.  (Not with k_fused, whose look-back granules k_stats zeroes.)
   const int nv0 = std::min(vpg, p0.n_views);
-  bool pre_use = c->pre_armed && decide && adaptive && !c->fused && p0.stack == c->pre_stack &&
+  bool pre_use = arms.armed && decide && adaptive && !c->fused && p0.stack == c->pre_stack &&
                  p0.stack_vs == c->pre_vs && nv0 == c->pre_views && p0.HW == c->pre_hw;
-  c->pre_armed = false;
-  const int pre_in = c->pre_buf;
-  const bool pre_run = c->decl_next && !c->no_pre && !c->fused && cloud_mode >= 0 && vec;
+  int pre_in = c->pre_buf;
+  const bool pre_run = arms.decl && !c->no_pre && !c->fused && cloud_mode >= 0 && vec;
   const bool pre_dec = pre_run && decide && c->pre_decode;  // ... in the last k_decode instead (A/B)
-  c->decl_next = false;
-  int pre_nv = 0;
-  int64_t pre_bpv = 0;
-  if (pre_run) {
-    pre_nv = std::min(vpg, c->decl_views);
+  // Within a call of several launch groups: group g's k_cloud also runs group
+  // g + 1's histogram pass (the same pre-stats workgroups), so only the first
+  // group can need a k_stats launch (SLGPU_PRE_GROUPS=0: every group its own, A/B)
+  const bool pre_groups = decide && adaptive && n_groups > 1 && !c->no_pre && !c->no_pre_groups && !c->fused &&
+                          cloud_mode >= 0 && vec;
+  // pre-stats workgroups per view of a pass over nv views: up to 8 per CU in
+  // all (one 16-pixel step per thread at config 2; measured 0.5-1 us faster
+  // per c2 step than k_stats' 2 per CU)
+  auto pre_bpv_of = [&](int nv) -> int64_t {
     const int64_t per_view = (p0.HW / 16 + kThreads - 1) / kThreads;
-    // up to 8 workgroups per CU (one 16-pixel step per thread at config 2):
-    // measured 0.5-1 us faster per c2 step than k_stats' 2 per CU
     const int64_t wgs = c->pre_wgs > 0 ? c->pre_wgs : 8 * c->n_cu;
-    pre_bpv = std::max<int64_t>(1, std::min<int64_t>(per_view, (wgs + pre_nv - 1) / pre_nv));
-    const int64_t words = static_cast<int64_t>(pre_nv) * kHistView;
+    return std::max<int64_t>(1, std::min<int64_t>(per_view, (wgs + nv - 1) / nv));
+  };
+  {
+    int64_t words = 0;
+    if (pre_run) words = static_cast<int64_t>(std::min(vpg, c->decl_views)) * kHistView;
+    if (pre_groups) words = std::max<int64_t>(words, static_cast<int64_t>(std::min(vpg, p0.n_views - vpg)) * kHistView);
     if (words > c->cap_pre) {  // (re)allocated zeroed: nothing left to take
       pre_use = false;
       for (int b = 0; b < 3; ++b) {
@@ -2686,32 +2712,35 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
   if (!c->prof_ev.empty() && kProfEv * (c->prof_n + 1) <= static_cast<int>(c->prof_ev.size()))
     ev = &c->prof_ev[kProfEv * c->prof_n++];
   // The pre-stats workgroups' arguments on launch parameters pc of a grid
-  // with nv rows: the launch grows by as many workgroups per row as they need
-  // (after its own), and the next call is armed for them.
-  auto add_pre = [&](Params& pc, dim3& grid, int nv) -> int {
+  // with nv rows, for the pnv views of stack pst (view stride pvs): the launch
+  // grows by as many workgroups per row as they need (after its own); the
+  // pass accumulates into buffer c->pre_buf, for the stack recorded in c->pre_*.
+  auto add_pre = [&](Params& pc, dim3& grid, int nv, const uint8_t* pst, int64_t pvs, int pnv) -> int {
     const int acc = c->pre_acc, zb = (acc + 1) % 3;
+    const int64_t bpv = pre_bpv_of(pnv);
     if (c->pre_dirty[acc] > 0)
       HIP_TRY(c, hipMemsetAsync(c->d_pre[acc], 0, sizeof(unsigned) * c->pre_dirty[acc], s));
-    pc.pre_stack = c->decl_stack;
-    pc.pre_vs = c->decl_vs;
+    pc.pre_stack = pst;
+    pc.pre_vs = pvs;
     pc.pre_hist = c->d_pre[acc];
     pc.pre_zero = c->d_pre[zb];
     pc.pre_zero_words = c->pre_dirty[zb];
-    pc.pre_views = pre_nv;
-    pc.pre_bpv = static_cast<int>(pre_bpv);
+    pc.pre_views = pnv;
+    pc.pre_bpv = static_cast<int>(bpv);
     pc.pre_mix = c->pre_mix;
-    const int64_t total = static_cast<int64_t>(pre_nv) * pre_bpv;
+    const int64_t total = static_cast<int64_t>(pnv) * bpv;
     grid.x += static_cast<unsigned>((total + nv - 1) / nv);
-    c->pre_dirty[acc] = static_cast<int64_t>(pre_nv) * kHistView;
+    c->pre_dirty[acc] = static_cast<int64_t>(pnv) * kHistView;
     c->pre_dirty[zb] = 0;
     c->pre_acc = zb;
     c->pre_buf = acc;
-    c->pre_stack = c->decl_stack;
-    c->pre_vs = c->decl_vs;
-    c->pre_views = pre_nv;
+    c->pre_stack = pst;
+    c->pre_vs = pvs;
+    c->pre_views = pnv;
     c->pre_hw = p0.HW;
     return SL_OK;
   };
+  bool next_pre = pre_use;  // the coming group's histograms were computed by the previous k_cloud
   int g = 0;  // launch group index
   for (int v0 = 0; v0 < p0.n_views; v0 += vpg, ++g) {
     hipEvent_t* gev = (ev && g < kProfGroups) ? ev + 4 * g : nullptr;
@@ -2744,7 +2773,8 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     // histograms it zeroes (the previous group's or call's k_decode) and, for
     // a call's first group, the caller's readiness event (else after
     // everything queued so far: the side path's first use)
-    const bool pre_g = pre_use && g == 0;  // histograms computed by the previous call's k_cloud
+    const bool pre_g = next_pre;  // histograms computed by the previous k_cloud (this call's or the last call's)
+    next_pre = false;
     const bool ahead = !pre_g && side_ok && ((g > 0 && c->side_groups) || (g == 0 && ready));
     hipStream_t ss = ahead ? c->side : s;
     if (g == 0 && ready_ev && !ahead) HIP_TRY(c, hipStreamWaitEvent(s, ready_ev, 0));  // the promise, kept on s
@@ -2850,7 +2880,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       dim3 pgrid = dgrid;
       if (pre_dec && g == n_groups - 1) {  // + the declared next call's histogram pass, in k_decode's tail
         pd.decode_gx = static_cast<int>(dgrid.x);
-        r = add_pre(pd, pgrid, nv);
+        r = add_pre(pd, pgrid, nv, c->decl_stack, c->decl_vs, std::min(vpg, c->decl_views));
         if (r) return r;
       }
       void* args[] = {&pd};
@@ -2882,14 +2912,24 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->last.fn[2] = reinterpret_cast<const void*>(fn);
       Params pc = p;
       dim3 cgrid = grid;
-      const bool pre_now = pre_run && !pre_dec && g == n_groups - 1;
+      const bool last_g = g == n_groups - 1;
+      const bool pre_now = pre_run && !pre_dec && last_g;
+      const bool pre_grp = pre_groups && !last_g;
       if (pre_now) {  // + the declared next call's histogram pass, after this group's triangulating workgroups
-        r = add_pre(pc, cgrid, nv);
+        r = add_pre(pc, cgrid, nv, c->decl_stack, c->decl_vs, std::min(vpg, c->decl_views));
+        if (r) return r;
+      } else if (pre_grp) {  // + this call's next launch group's
+        r = add_pre(pc, cgrid, nv, p0.stack + static_cast<int64_t>(v0 + vpg) * p0.stack_vs, p0.stack_vs,
+                    std::min(vpg, p0.n_views - v0 - vpg));
         if (r) return r;
       }
       void* args[] = {&pc};
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), cgrid, dim3(kThreads), args, 0, s));
       if (pre_now) c->pre_armed = true;
+      if (pre_grp) {
+        next_pre = true;
+        pre_in = c->pre_buf;
+      }
     }
     if (gev) HIP_TRY(c, hipEventRecord(gev[3], s));
   }
@@ -3065,6 +3105,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
   if (const char* d = getenv("SLGPU_XY_CALC")) c->xy_calc_env = atoi(d) != 0;
   if (const char* d = getenv("SLGPU_FUSED")) c->fused = atoi(d) != 0;
   if (const char* d = getenv("SLGPU_PRESTATS")) c->no_pre = atoi(d) == 0;
+  if (const char* d = getenv("SLGPU_PRE_GROUPS")) c->no_pre_groups = atoi(d) == 0;
   if (const char* d = getenv("SLGPU_PRE_MIX")) c->pre_mix = atoi(d);
   if (const char* d = getenv("SLGPU_PRE_WGS")) c->pre_wgs = std::max(0, atoi(d));
   if (const char* d = getenv("SLGPU_PRE_DECODE")) c->pre_decode = atoi(d) != 0;
@@ -3314,6 +3355,7 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   const hipEvent_t ready_ev = c->ready_ev_next;
   c->ready_next = false;
   c->ready_ev_next = nullptr;
+  const PreArms arms = take_arms(c);  // sl_stack_next's declaration, a queued pre-stats pass (likewise)
   int r = common_out_checks(c, n_views, H, W, xyz, xyz_dtype, bgr, cap, view_offsets);
   if (r) return r;
   if (!stack) return fail(c, SL_EINVAL, "stack is NULL");
@@ -3378,8 +3420,8 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   const hipStream_t s = static_cast<hipStream_t>(stream);
   r = stream_handoff(c, s);
   if (r) return r;
-  return launch(c, p, vec, decide ? (decode_mode | M_DECIDE) : decode_mode, count_mode, cloud_mode, s, ready,
-                ready_ev);
+  return launch(c, p, vec, decide ? (decode_mode | M_DECIDE) : decode_mode, count_mode, cloud_mode, s, arms,
+                ready, ready_ev);
 }
 
 int sl_stack_ready(sl_ctx* c, void* event) {
@@ -3453,6 +3495,7 @@ int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, 
                         int n_views, int H, int W, const double* poses, void* xyz, int xyz_dtype,
                         uint8_t* bgr, int64_t cap, int64_t* view_offsets, void* stream) {
   if (!c) return SL_EINVAL;
+  const PreArms arms = take_arms(c);  // (consumed even on failure, as sl_decode_triangulate's)
   if (!xyz) return fail(c, SL_EINVAL, "xyz_out is NULL");
   int r = common_out_checks(c, n_views, H, W, xyz, xyz_dtype, bgr, cap, view_offsets);
   if (r) return r;
@@ -3477,7 +3520,7 @@ int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, 
   const hipStream_t s = static_cast<hipStream_t>(stream);
   r = stream_handoff(c, s);
   if (r) return r;
-  return launch(c, p, vec, decode_mode, count_mode, cloud_mode, s);
+  return launch(c, p, vec, decode_mode, count_mode, cloud_mode, s, arms);
 }
 
 int sl_mask_counts_to(sl_ctx* c, int64_t* device_counts) {

@@ -1887,8 +1887,8 @@ int sl_estimate_normals(sl_ctx* c, const double* xyz, int64_t n, double radius, 
 
 // registration_icp with TransformationEstimationPointToPlane (processing.py:
 // 154-156).  Host side of each iteration: the block partials folded left to
-// right, the 6x6 normal equations JTJ x = -JTr by Cholesky (Open3D: Eigen
-// LDLT; identity when not positive definite), x = (alpha, beta, gamma, t) ->
+// right, the 6x6 normal equations JTJ x = -JTr by a pivoted LDLT (Open3D:
+// Eigen's LDLT, icp_update), x = (alpha, beta, gamma, t) ->
 // update = [Rz(gamma) Ry(beta) Rx(alpha) | t] (TransformVector6dToMatrix4d),
 // transformation = update * transformation, source moved by update.
 namespace {
@@ -1907,34 +1907,70 @@ void icp_mat4(const double* a, const double* b, double* o) {  // row-major 4x4: 
 }
 
 // 6x6 JTJ x = -JTr (sums: JTJ upper triangle row-major, then JTr) -> update
-// (row-major 4x4); false (identity update) when JTJ is not positive definite
+// (row-major 4x4), as Open3D's SolveLinearSystemPSD (utility/Eigen.cpp: no
+// PSD / determinant checks, x = A.ldlt().solve(b)) -- Eigen's LDLT: the
+// unblocked left-looking factorisation with diagonal pivoting (the largest
+// |a_ii| of the not yet factored diagonal, first on ties), pivots of 0 left
+// unscaled, and a solve that zeroes the components of |d_i| <= DBL_MIN (its
+// pseudo-inverse of D), so a rank-deficient system still moves along the
+// directions it constrains.  Sums of products run left to right (Eigen's
+// vectorised order may differ in the last bits; parity with Open3D unpinned).
+// false (identity update) only when the solution is not finite.
 bool icp_update(const double* sums, double* update) {
-  double A[6][6], L[6][6] = {}, y[6], x[6], bb[6];
+  double F[6][6], b[6], x[6], tmp[6];
+  int tr[6];
   int k = 0;
   for (int a = 0; a < 6; ++a)
-    for (int c = a; c < 6; ++c, ++k) A[a][c] = A[c][a] = sums[k];
-  for (int a = 0; a < 6; ++a) bb[a] = -sums[21 + a];
+    for (int c = a; c < 6; ++c, ++k) F[a][c] = F[c][a] = sums[k];
+  for (int a = 0; a < 6; ++a) b[a] = -sums[21 + a];
   for (int i = 0; i < 16; ++i) update[i] = (i % 5 == 0) ? 1.0 : 0.0;
+  bool zero_all = false;
   for (int j = 0; j < 6; ++j) {
-    double d = A[j][j];
-    for (int q = 0; q < j; ++q) d = d - L[j][q] * L[j][q];
-    if (!(d > 0.0) || !std::isfinite(d)) return false;
-    L[j][j] = std::sqrt(d);
-    for (int i = j + 1; i < 6; ++i) {
-      double v = A[i][j];
-      for (int q = 0; q < j; ++q) v = v - L[i][q] * L[j][q];
-      L[i][j] = v / L[j][j];
+    int p = j;
+    for (int i = j + 1; i < 6; ++i)
+      if (std::fabs(F[i][i]) > std::fabs(F[p][p])) p = i;
+    tr[j] = p;
+    if (p != j) {  // symmetric swap of rows / columns j and p (full storage)
+      for (int q = 0; q < 6; ++q) std::swap(F[j][q], F[p][q]);
+      for (int q = 0; q < 6; ++q) std::swap(F[q][j], F[q][p]);
     }
+    if (j > 0) {
+      for (int q = 0; q < j; ++q) tmp[q] = F[q][q] * F[j][q];
+      double d = 0.0;
+      for (int q = 0; q < j; ++q) d = d + F[j][q] * tmp[q];
+      F[j][j] = F[j][j] - d;
+      for (int i = j + 1; i < 6; ++i) {
+        double v = 0.0;
+        for (int q = 0; q < j; ++q) v = v + F[i][q] * tmp[q];
+        F[i][j] = F[i][j] - v;
+      }
+    }
+    const double piv = F[j][j];
+    if (j == 0 && !(std::fabs(piv) > 0.0)) {  // the whole diagonal is 0: A = 0, x = 0
+      zero_all = true;
+      break;
+    }
+    if (std::fabs(piv) > 0.0)
+      for (int i = j + 1; i < 6; ++i) F[i][j] = F[i][j] / piv;
   }
-  for (int i = 0; i < 6; ++i) {
-    double v = bb[i];
-    for (int q = 0; q < i; ++q) v = v - L[i][q] * y[q];
-    y[i] = v / L[i][i];
-  }
-  for (int i = 5; i >= 0; --i) {
-    double v = y[i];
-    for (int q = i + 1; q < 6; ++q) v = v - L[q][i] * x[q];
-    x[i] = v / L[i][i];
+  if (zero_all) {
+    for (int i = 0; i < 6; ++i) x[i] = 0.0;
+  } else {
+    for (int j = 0; j < 6; ++j) std::swap(b[j], b[tr[j]]);  // P b
+    for (int i = 0; i < 6; ++i) {                            // L^-1 (unit lower)
+      double v = 0.0;
+      for (int q = 0; q < i; ++q) v = v + F[i][q] * b[q];
+      b[i] = b[i] - v;
+    }
+    for (int i = 0; i < 6; ++i)  // D^+
+      b[i] = std::fabs(F[i][i]) > std::numeric_limits<double>::min() ? b[i] / F[i][i] : 0.0;
+    for (int i = 5; i >= 0; --i) {  // L^-T
+      double v = 0.0;
+      for (int q = i + 1; q < 6; ++q) v = v + F[q][i] * b[q];
+      b[i] = b[i] - v;
+    }
+    for (int j = 5; j >= 0; --j) std::swap(b[j], b[tr[j]]);  // P^T
+    for (int i = 0; i < 6; ++i) x[i] = b[i];
   }
   for (int i = 0; i < 6; ++i)
     if (!std::isfinite(x[i])) return false;
@@ -1959,9 +1995,10 @@ int sl_icp_point_to_plane(sl_ctx* c, const double* source, int64_t n_src, const 
                           const double* target_normals, int64_t n_tgt, double max_distance, const double* init,
                           int max_iteration, double relative_fitness, double relative_rmse, double* transformation,
                           double* fitness, double* inlier_rmse, int* iterations, void* stream) {
-  if (!c || n_src < 0 || n_tgt < 0 || !init || !transformation || max_iteration < 0 ||
-      (n_src && !source) || (n_tgt && (!target || !target_normals)))
-    return SL_EINVAL;
+  if (!c) return SL_EINVAL;
+  if (n_src < 0 || n_tgt < 0 || !init || !transformation || max_iteration < 0 || (n_src && !source) ||
+      (n_tgt && (!target || !target_normals)))
+    return slgpu_fail(c, SL_EINVAL, "sl_icp_point_to_plane: bad sizes or NULL arguments");
   if (n_src >= (1ll << 31) || n_tgt >= (1ll << 31)) return slgpu_fail(c, SL_EINVAL, "at most 2^31 - 1 points");
   if (!(max_distance > 0.0)) return slgpu_fail(c, SL_EINVAL, "max_correspondence_distance must be > 0");
   double T[16];
@@ -1999,11 +2036,13 @@ int sl_icp_point_to_plane(sl_ctx* c, const double* source, int64_t n_src, const 
   DBuf<int32_t> corr, dense;
   MTRY(c, sxyz.alloc(3 * n_tgt));
   hipLaunchKernelGGL(k_gather_sorted, dim3(blocks(n_tgt)), dim3(kT), 0, s, target, idx.p, n_tgt, sxyz.p);
+  MTRY(c, hipGetLastError());
   const int64_t ncell = (g.nx * g.ny) * g.nz;
   if (ncell <= (int64_t{1} << 26)) {  // a dense cell table (<= 256 MB), else binary search
     MTRY(c, dense.alloc(ncell));
     MTRY(c, hipMemsetAsync(dense.p, 0xff, sizeof(int32_t) * ncell, s));
     hipLaunchKernelGGL(k_icp_dense, dim3(blocks(m)), dim3(kT), 0, s, ukeys.p, m, dense.p);
+    MTRY(c, hipGetLastError());
   }
   const int64_t nb = (n_src + kIcpBlock - 1) / kIcpBlock;
   MTRY(c, cur.alloc(3 * n_src));
@@ -2045,7 +2084,7 @@ int sl_icp_point_to_plane(sl_ctx* c, const double* source, int64_t n_src, const 
   if ((r = evaluate())) return r;
   for (int it = 0; it < max_iteration; ++it) {
     double U[16];
-    icp_update(sums, U);  // identity where the system is singular
+    icp_update(sums, U);  // (identity only for a non-finite solution)
     icp_mat4(U, T, T);
     if ((r = move(U))) return r;
     const double f0 = fit, r0 = rmse;

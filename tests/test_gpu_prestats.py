@@ -107,7 +107,7 @@ def test_chained_calls_without_syncs(env, monkeypatch):
 def test_chained_multi_group_calls():
     """Calls of two launch groups (34 1080p views: 32 + 2): the last group's
     k_cloud computes the histograms of the next call's first group (32 views);
-    that call's second group runs its own k_stats."""
+    within each call the first group's k_cloud computes the second group's."""
     from structured_light_for_3d_model_replication_amd import core, synth
     H, W, V = 1080, 1920, 34
     rig = synth.Rig(H=H, W=W)
@@ -244,3 +244,146 @@ def test_graph_captured_chain():
     torch.cuda.synchronize()
     _same(_snap(r, eng)[:-1], ref[:-1], "eager after replay")
     _same(_snap(r2, eng)[:-1], ref[:-1], "after drop_next")
+
+
+def _group_views(H, W, V, maps, seed0):
+    """V resident views cycling through 3 rendered ones (stack, texture), the
+    3 base views, and their single-view clouds/maps (one launch group each)."""
+    from structured_light_for_3d_model_replication_amd import synth
+    rig = synth.Rig(H=H, W=W)
+    base = [synth.render_stack(rig, seed=seed0 + v, view_deg=50.0 * v, device="cuda", include_rows=maps)
+            for v in range(3)]
+    n_img = base[0][0].shape[0]
+    A = torch.empty((V, n_img, H, W), dtype=torch.uint8, device="cuda")
+    TA = torch.empty((V, H, W, 3), dtype=torch.uint8, device="cuda")
+    for v in range(V):
+        A[v].copy_(base[v % 3][0])
+        TA[v].copy_(base[v % 3][1])
+    return rig, base, A, TA
+
+
+@pytest.mark.parametrize("maps", [False, True])
+def test_multi_group_call_prestats_between_groups(maps, monkeypatch):
+    """One call of three launch groups (70 1080p views: 32 + 32 + 6): groups 2
+    and 3 take the histograms the previous group's k_cloud computed (no k_stats
+    launch).  Every view's thresholds, cloud slice (and maps) equal those of
+    the same view decoded alone; the whole output equals a context with the
+    pass between groups switched off (SLGPU_PRE_GROUPS=0, A/B); one view of the
+    last group against the oracle."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W, V = 1080, 1920, 70
+    rig, base, A, TA = _group_views(H, W, V, maps, 300)
+    cal = synth.make_calibration(rig, with_Nc=False)
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    single = []
+    for st, tx in base:
+        r = eng.decode_triangulate(st, texture=tx, maps=maps, cloud=True, xyz_dtype=torch.float32, out={})
+        eng.sync()
+        single.append(_snap(r, eng))
+    kw = dict(texture=TA, maps=maps, cloud=True, xyz_dtype=torch.float32)
+    r = eng.decode_triangulate(A, out={}, **kw)
+    eng.sync()
+    assert eng.last_launch_info()[1] == 3
+    got = _snap(r, eng)[:-1]
+    off = got[2]
+    for v in range(V):
+        ref = single[v % 3]
+        n = ref[2][1]
+        np.testing.assert_array_equal(got[0][off[v]:off[v + 1]], ref[0][:n], err_msg=f"view {v} xyz")
+        np.testing.assert_array_equal(got[1][off[v]:off[v + 1]], ref[1][:n], err_msg=f"view {v} bgr")
+        if maps:
+            for k in (3, 4, 5):
+                np.testing.assert_array_equal(got[k][v], ref[k][0], err_msg=f"view {v} map {k}")
+        np.testing.assert_array_equal(np.array(eng.last_thresholds(v), dtype=np.float64), ref[-1],
+                                      err_msg=f"view {v} thresholds")
+    monkeypatch.setenv("SLGPU_PRE_GROUPS", "0")
+    eng0 = core.Reconstructor(torch.device("cuda", 0))
+    eng0.set_calibration(cal, H, W)
+    r0 = eng0.decode_triangulate(A, out={}, **kw)
+    eng0.sync()
+    _same(got, _snap(r0, eng0)[:-1], "SLGPU_PRE_GROUPS=0")
+    v = 67  # last group
+    col, row, mask, P, C = o.decode_triangulate(list(A[v].cpu().numpy()), TA[v].cpu().numpy(), cal)
+    np.testing.assert_array_equal(got[0][off[v]:off[v + 1]], P.astype(np.float32))
+    np.testing.assert_array_equal(got[1][off[v]:off[v + 1]], C)
+
+
+def test_failed_call_consumes_queued_pass():
+    """call N queues the pass for stack B (next_stack=B); call N+1
+    on B fails its argument checks (in C); the caller refills B with other
+    images; call N+2 on B must compute its own histograms -- not take the
+    queued ones of B's old contents."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 480, 640
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    sa, ta = synth.render_stack(rig, seed=21, view_deg=0.0, device="cuda")
+    sb, tb = synth.render_stack(rig, seed=22, view_deg=30.0, device="cuda")
+    sc, tc = synth.render_stack(rig, seed=23, view_deg=60.0, device="cuda")
+    sc[1].add_(40)  # a brighter black plane: other thresholds than B's
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    kw = dict(maps=True, cloud=True, xyz_dtype=torch.float32)
+    ref_c = _snap(eng.decode_triangulate(sc, texture=tc, out={}, **kw), eng)
+    eng.sync()
+    ref_b = _snap(eng.decode_triangulate(sb, texture=tb, out={}, **kw), eng)
+    eng.sync()
+    assert not np.array_equal(ref_b[-1], ref_c[-1]), "the test needs B and C to have other thresholds"
+    B, TB = sb.clone(), tb.clone()
+    eng.decode_triangulate(sa, texture=ta, out={}, next_stack=B, **kw)
+    with pytest.raises(ValueError):
+        eng.decode_triangulate(B, 70000, texture=TB, out={}, **kw)  # n_cols > 65536: EINVAL in C
+    eng.sync()
+    B.copy_(sc)
+    TB.copy_(tc)
+    r = eng.decode_triangulate(B, texture=TB, out={}, **kw)
+    eng.sync()
+    _same(_snap(r, eng), ref_c, "refilled B after a failed chained call")
+
+
+def test_failed_arming_leaves_counts_alone():
+    """mask_counts plus a bad next_stack raises before anything is
+    armed; the next plain call leaves that counts tensor untouched (and a
+    C-side failure consumes an armed counts pointer too)."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 96, 128
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    st, tx = synth.render_stack(rig, seed=2, device="cuda")
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    counts = torch.full((1,), -7, dtype=torch.int64, device="cuda")
+    flat = torch.empty(st.numel() + 1, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        eng.decode_triangulate(st, texture=tx, mask_counts=counts, next_stack=flat[1:].view(st.shape))
+    eng.decode_triangulate(st, texture=tx)
+    eng.sync()
+    assert counts.item() == -7
+    with pytest.raises(ValueError):
+        eng.decode_triangulate(st, 70000, texture=tx, mask_counts=counts)
+    eng.decode_triangulate(st, texture=tx)
+    eng.sync()
+    assert counts.item() == -7
+    good = torch.zeros(1, dtype=torch.int64, device="cuda")
+    r = eng.decode_triangulate(st, texture=tx, maps=True, mask_counts=good)
+    eng.sync()
+    assert good.item() == int(r["mask"].sum().item())
+
+
+def test_prepared_call_after_close_raises():
+    """Reconstructor.close() closes its prepared calls; running one
+    afterwards raises instead of touching a freed context."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 96, 128
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    st, tx = synth.render_stack(rig, seed=3, device="cuda")
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    pc = eng.prepare(st, texture=tx, cloud=True, out={})
+    pc.run()
+    eng.sync()
+    eng.close()
+    with pytest.raises(RuntimeError):
+        pc.run()
