@@ -128,6 +128,16 @@ def parse(argv=None):
                          "(untimed) right after the pre-roll -- every kernel of every step runs, the host enqueues "
                          "nothing inside the window (default; falls back to eager calls if capture fails)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
+    ap.add_argument("--verify", dest="verify", action="store_true", default=True,
+                    help="after the windows, check the last timed step's outputs of a sample of views (the first "
+                         "and the last of this rank) against the oracle run on the same resident inputs (default)")
+    ap.add_argument("--no-verify", dest="verify", action="store_false")
+    ap.add_argument("--single-shot", dest="single_shot", type=int, default=24,
+                    help="isolated unchained calls timed for the one-shot latency block (0: off)")
+    ap.add_argument("--strong-leg", dest="strong_leg", action="store_true", default=True,
+                    help="N > 1: also time BASELINE config 3 strong-scaled (36 views sharded over the N ranks) "
+                         "and report it in multi_gpu.strong_c3 (default)")
+    ap.add_argument("--no-strong-leg", dest="strong_leg", action="store_false")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r03_traffic_c2.json"),
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
                          "scripts/traffic_from_pmc.py)")
@@ -242,6 +252,14 @@ def selftest(a) -> None:
         return counts
     rep = gather_report(el, xyz.shape[0], 15, torch.device("cpu"), gfn, distributed)
     xa = got.get("xa", xyz)
+    if distributed and a.strong_leg:
+        # the strong-scaled config-3 leg's plumbing: 36 views sharded, stand-in clouds
+        def leg_step(views3):
+            return torch.cat([torch.full((n_per_view, 3), float(v), dtype=torch.float32) for v in views3]) \
+                if views3 else torch.zeros((0, 3), dtype=torch.float32)
+        rep["strong_c3"] = strong_leg_report(
+            a, world, rank, distributed, torch.device("cpu"), px_per_view=1920 * 1080,
+            run=lambda views3: _stand_in_leg(a, views3, leg_step))
     if rank == 0:
         order_ok = bool(torch.equal(xa[::n_per_view, 0], torch.arange(xa.shape[0] // n_per_view,
                                                                       dtype=torch.float32)))
@@ -251,6 +269,200 @@ def selftest(a) -> None:
                           "view_order_ok": order_ok, "max_rank_s": float(t.item()), "multi_gpu": rep}))
     if distributed:
         dist.destroy_process_group()
+
+
+def _stand_in_leg(a, views3, leg_step):
+    """selftest: the strong leg's K steps on stand-in clouds -> (seconds, xyz, bgr)."""
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        xyz = leg_step(views3)
+    el = time.perf_counter() - t0
+    return el, xyz, torch.zeros((xyz.shape[0], 3), dtype=torch.uint8)
+
+
+def strong_leg_report(a, world, rank, distributed, device, px_per_view, run, V=36):
+    """BASELINE config 3 as the N-GPU run's second line: V views in total,
+    sharded over the ranks (parallel.shard_views, view v -> rank
+    floor(v*G/V)); run(views) -> (this rank's seconds for the K steps after a
+    barrier, xyz, bgr of its last step); then the same multi-rank report and
+    timed gather to rank 0 as the headline's."""
+    views3 = list(parallel.shard_views(V, world, rank))
+    if distributed:
+        dist.barrier()
+    el, xyz, bgr = run(views3)
+
+    def gfn():
+        _, _, counts = parallel.gather_cloud(xyz, bgr, dst=0)
+        return counts
+    rep = gather_report(el, xyz.shape[0], 15 if xyz.dtype == torch.float32 else 27, device, gfn, distributed)
+    per_views = [len(parallel.shard_views(V, world, r)) for r in range(world)]
+    t_max = max(rep["per_rank_s"])
+    rep.update({"config": f"BASELINE config 3: {V} x 1920x1080 views in total, sharded over {world} rank(s) "
+                          "(strong scaling), cloud only, exact xyz",
+                "views_total": V, "per_rank_views": per_views, "steps": a.steps,
+                "per_rank_ms_per_step": [1e3 * t / a.steps for t in rep["per_rank_s"]],
+                "ms_per_step": 1e3 * t_max / a.steps,
+                "px_per_s": V * px_per_view * a.steps / t_max if t_max > 0 else None})
+    return rep
+
+
+def single_shot(eng, call, n, stream):
+    """One-shot latency (the GUI's generate_cloud: one call at a time,
+    sl_system.py:655-661): ``n`` isolated calls -- synchronize, enqueue one
+    unchained call (its own k_stats included), synchronize -- after two
+    untimed ones; host wall µs and HIP-event µs on the call's stream."""
+    eng.drop_next()  # no pass queued by an earlier chained call is taken
+    wall, gpu = [], []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for i in range(n + 2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(stream)
+        call()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if i >= 2:
+            wall.append(1e6 * (t1 - t0))
+            gpu.append(1e3 * e0.elapsed_time(e1))
+    return {"calls": n, "wall_us": spread(wall), "gpu_us": spread(gpu)}
+
+
+def run_c3_leg(a, dev, views3):
+    """The strong leg on the GPU: this rank's shard of config 3's views,
+    resident, through config 3's lanes (CONFIGS["c3"]), chained as the
+    headline; warm-up, a 100-ms pre-roll, then K steps between synchronizes
+    -> (seconds, xyz, bgr of lane 0's last step)."""
+    cfg = CONFIGS["c3"]
+    H, W = cfg["H"], cfg["W"]
+    rig = synth.Rig(H=H, W=W, Wp=cfg["Wp"], Hp=cfg["Hp"])
+    calib = synth.make_calibration(rig, with_Nc=False)
+    stack = tex = None
+    for k, gv in enumerate(views3):
+        s_, t_ = synth.render_stack(rig, seed=1000 * 3 + gv, include_rows=True, view_deg=cfg["deg"] * gv, device=dev)
+        if stack is None:
+            stack = torch.empty((len(views3),) + tuple(s_.shape), dtype=torch.uint8, device=dev)
+            tex = torch.empty((len(views3), H, W, 3), dtype=torch.uint8, device=dev)
+        stack[k].copy_(s_)
+        tex[k].copy_(t_)
+        del s_, t_
+    pool = core.ReconstructorPool(dev, lanes=cfg["streams"], reuse_outputs=True)
+    pool.set_calibration(calib, H, W)
+
+    def one():
+        pool.decode_triangulate(stack, cfg["Wp"], cfg["Hp"], texture=tex, maps=False, cloud=True,
+                                xyz_dtype=torch.float32, wait_inputs=False, next_stack=stack)
+    if stack is not None:
+        for _ in range(max(a.warmup, pool.lanes)):
+            one()
+        torch.cuda.synchronize(dev)
+        t_pr = time.perf_counter()
+        while (time.perf_counter() - t_pr) * 1e3 < min(a.preroll_ms, 100.0):
+            for _ in range(4):
+                one()
+            torch.cuda.synchronize(dev)
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if stack is not None:
+        for _ in range(a.steps):
+            one()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if stack is None:
+        xyz, bgr = torch.zeros((0, 3), dtype=torch.float32, device=dev), torch.zeros((0, 3), dtype=torch.uint8, device=dev)
+    else:
+        o = pool._outs[0]
+        n = int(o["view_offsets"][-1].item())
+        xyz, bgr = o["xyz"][:n], o["bgr"][:n]
+    return el, xyz, bgr
+
+
+def single_shot_c1(dev, n, stream):
+    """single_shot of BASELINE config 1's view (1280x720, 10 column bits,
+    maps + cloud) on a context of its own."""
+    cfg = CONFIGS["c1"]
+    rig = synth.Rig(H=cfg["H"], W=cfg["W"], Wp=cfg["Wp"], Hp=cfg["Hp"])
+    st, tx = synth.render_stack(rig, seed=1000, include_rows=False, device=dev)
+    e = core.Reconstructor(dev)
+    e.set_calibration(synth.make_calibration(rig, with_Nc=False), cfg["H"], cfg["W"])
+    o = {}
+
+    def call():
+        e.decode_triangulate(st, cfg["Wp"], cfg["Hp"], texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32,
+                             out=o, stream=stream)
+    r = single_shot(e, call, n, stream)
+    e.close()
+    return r
+
+
+def snap_alloc(out, V, maps):
+    """Pinned host buffers for the outputs of views 0 and V-1 (the verified
+    sample), sized from the warm-up's offsets (the same inputs every step)."""
+    vo = out["view_offsets"].cpu().numpy()
+    pin = dict(pin_memory=True)
+    snap = {"vo": vo, "vo_dev": torch.empty(V + 1, dtype=torch.int64, **pin), "views": {}}
+    for v in sorted({0, V - 1}):
+        n = int(vo[v + 1] - vo[v])
+        d = {"xyz": torch.empty((n, 3), dtype=out["xyz"].dtype, **pin), "bgr": torch.empty((n, 3), dtype=torch.uint8, **pin)}
+        if maps:
+            d.update(col=torch.empty(out["col_map"].shape[1:], dtype=torch.int32, **pin),
+                     row=torch.empty(out["row_map"].shape[1:], dtype=torch.int32, **pin),
+                     mask=torch.empty(out["mask_u8"].shape[1:], dtype=torch.uint8, **pin))
+        snap["views"][v] = d
+    return snap
+
+
+def snap_copy(snap, out, stream):
+    """Enqueue the copies of the current outputs into the pinned buffers on
+    ``stream`` (right after the headline window: they hold its last step's)."""
+    vo = snap["vo"]
+    with torch.cuda.stream(stream):
+        snap["vo_dev"].copy_(out["view_offsets"], non_blocking=True)
+        for v, d in snap["views"].items():
+            d["xyz"].copy_(out["xyz"][vo[v]:vo[v + 1]], non_blocking=True)
+            d["bgr"].copy_(out["bgr"][vo[v]:vo[v + 1]], non_blocking=True)
+            if "col" in d:
+                d["col"].copy_(out["col_map"][v], non_blocking=True)
+                d["row"].copy_(out["row_map"][v], non_blocking=True)
+                d["mask"].copy_(out["mask_u8"][v], non_blocking=True)
+
+
+def verify(snap, stack, tex, poses, calib, n_cols, n_rows, fast):
+    """The snapshot (the last timed step's outputs) against the oracle
+    (oracle/sl_oracle.py: the reference's gray_decode + reconstruct_point_cloud,
+    sl_system.py:508-653) run on the same resident inputs: maps, mask, point
+    count and colours bit-exact; xyz = float32 of the oracle's f64 (exact
+    mode) or within 1.02e-5 relative per coordinate (fast mode)."""
+    from oracle import sl_oracle
+    t0 = time.perf_counter()
+    ok = bool(np.array_equal(snap["vo_dev"].numpy(), snap["vo"]))  # the window's offsets = the warm-up's
+    notes = []
+    for v, dt in snap["views"].items():
+        d = {k: t.numpy() for k, t in dt.items()}
+        if "mask" in d:
+            d["mask"] = d["mask"].astype(bool)
+        st = stack[v].cpu().numpy()
+        tx = tex[v].cpu().numpy()
+        pose = None if poses is None else poses[v].cpu().numpy().reshape(4, 4)
+        col, row, mask, P, C = sl_oracle.decode_triangulate(list(st), tx, calib, n_cols, n_rows, pose=pose)
+        good = len(P) == len(d["xyz"]) and np.array_equal(d["bgr"], C)
+        if good and fast:
+            P32 = P.astype(np.float32)
+            good = bool(np.all(np.abs(d["xyz"].astype(np.float64) - P) <= 1.02e-5 * np.abs(P) + 1e-30)) and \
+                bool(np.isfinite(P32).all())
+        elif good:
+            good = np.array_equal(d["xyz"].view(np.uint32), P.astype(np.float32).view(np.uint32))
+        if "col" in d:
+            good = good and np.array_equal(d["col"], col) and np.array_equal(d["row"], row) and \
+                np.array_equal(d["mask"], mask)
+        notes.append({"view": int(v), "points": int(len(P)), "equal": bool(good)})
+        ok = ok and good
+    return ok, {"views": notes, "oracle_s": time.perf_counter() - t0,
+                "what": "the last timed step's maps, mask, point count, xyz and BGR of views 0 and V-1 vs "
+                        "oracle/sl_oracle.py on the same resident stacks: " +
+                        ("xyz within 1.02e-5 rel (fast mode)" if fast else "xyz == float32(reference f64), bitwise")}
 
 
 def path_bytes(H, W, read_planes, n_points, maps):
@@ -583,6 +795,7 @@ def main():
     # the headline window has none; an identical window with one event per
     # step boundary follows immediately and gives the per-step spread.
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+    snap = snap_alloc(out, V, maps) if a.verify else None
     gc.collect()
     gc.disable()
     try:
@@ -603,6 +816,8 @@ def main():
         else:
             el_rank, _ = timed(a.steps)
         enq_ms = host_enq_ms[0]
+        if snap is not None:  # the headline window's last step (the next window's sync waits for the copies)
+            snap_copy(snap, out, cur)
         el_ev, step_us = timed(a.steps, evs)
     finally:
         gc.enable()
@@ -626,6 +841,9 @@ def main():
     if distributed:
         multi["gather_path"] = ("sl_gather (the library's RCCL communicator)" if a.gather == "native"
                                 else "torch.distributed batch_isend_irecv (RCCL)")
+    if distributed and a.strong_leg and not (a.config == "c3" and a.scaling == "strong"):
+        multi["strong_c3"] = strong_leg_report(a, world, rank, distributed, dev, 1920 * 1080,
+                                               lambda views3: run_c3_leg(a, dev, views3))
 
     # per-kernel time: HIP events recorded by the library on the launch stream
     # around k_stats / k_decode / k_cloud, in a separate pass (events between
@@ -679,6 +897,33 @@ def main():
                "ms_per_step": 1e3 * el_alt / a.steps, "k_cloud_ms": acloud_ms / max(anl, 1),
                "note": "secondary: never the headline" if not head_fast else "the reference's arithmetic"}
         del o3
+
+    # one-shot latency: the config's call as the GUI makes it (unchained, one
+    # at a time), and config 1's single view beside a config-2 run
+    shots = None
+    if a.single_shot > 0 and rank == 0:
+        e1, s1 = (eng, cur) if pool is None else (pool.engines[0], pool.streams[0])
+        o_ss = out  # (its verified sample was copied out after the headline window)
+
+        def call_cfg():
+            e1.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
+                                  xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast, out=o_ss, stream=s1)
+        shots = {a.config: single_shot(e1, call_cfg, a.single_shot, s1)}
+        if a.config == "c2":
+            shots["c1"] = single_shot_c1(dev, a.single_shot, cur)
+        shots["note"] = ("isolated calls (synchronize, one unchained call with its own k_stats, synchronize), "
+                         "stacks resident; wall_us = host enqueue + GPU + sync latency, gpu_us = HIP events "
+                         "around the call on its stream; the headline instead streams chained calls")
+        del o_ss
+
+    verified, verification = None, None
+    if snap is not None:
+        verified, verification = verify(snap, stack, tex, poses, calib, n_cols, n_rows, head_fast)
+        if distributed:
+            f = torch.tensor([1 if verified else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            verified = bool(f.item())
+            verification["ranks"] = world
 
     cpu = cpu_baseline_single(a, cfg, cfg_idx, cpu_multi) if cpu_on else None
 
@@ -776,6 +1021,9 @@ def main():
                                                      "kernels after k_decode fit the 256 MB Infinity Cache, so "
                                                      "theirs run warm"}},
             "cpu_baseline": cpu,
+            "verified": verified,
+            "verification": verification,
+            "single_shot": shots,
             "points_per_view": n_pts / V,
             "cloud_only_px_per_s": None if el_cloud is None else px_step * a.steps / el_cloud,
             "multi_gpu": multi,

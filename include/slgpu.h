@@ -294,8 +294,11 @@ int sl_estimate_normals(sl_ctx* ctx, const double* xyz, int64_t n, double radius
  * 154-156), Open3D's RegistrationICP loop: every (moved) source point's
  * nearest target point with ((dx^2 + dy^2) + dz^2) < max_distance^2 (least
  * (d^2, index)); the point-to-plane step from those correspondences (JTJ and
- * JTr folded in source order, 64-point blocks left to right; 6x6 Cholesky;
- * update = [Rz Ry Rx | t] of the solution); transformation = update *
+ * JTr folded in source order, 64-point blocks left to right; the 6x6 system
+ * by a pivoted LDLT as Eigen's (Open3D's A.ldlt().solve(b): zero pivots give
+ * zero components, so a rank-deficient system still moves along the
+ * directions it constrains); update = [Rz Ry Rx | t] of the solution);
+ * transformation = update *
  * transformation; until |d fitness| < relative_fitness and |d rmse| <
  * relative_rmse, or max_iteration steps (Open3D's defaults: 30, 1e-6, 1e-6).
  * source / target / target_normals: device f64 [n][3]; init and the returned
@@ -307,6 +310,60 @@ int sl_icp_point_to_plane(sl_ctx* ctx, const double* source, int64_t n_src, cons
                           const double* target_normals, int64_t n_tgt, double max_distance, const double* init,
                           int max_iteration, double relative_fitness, double relative_rmse, double* transformation,
                           double* fitness, double* inlier_rmse, int* iterations, void* stream);
+
+/* ---- global registration (merge_pro_360's FPFH + RANSAC, processing.py:79-113) ----
+ * Open3D's algorithms restated (parity unpinned: no Open3D in this image;
+ * oracle/registration_oracle.py is the CPU restatement, bit-identical).
+ *
+ * KDTreeFlann::SearchHybrid(p, radius, max_nn) of every point of xyz [n][3]
+ * (device f64): the points with ((dx^2 + dy^2) + dz^2) < radius^2 (itself
+ * included) in ascending (d2, index), the first max_nn -> out_idx /
+ * out_d2 [n][max_nn] and out_cnt [n] (device).  max_nn <= 1024.  Blocking. */
+int sl_radius_search(sl_ctx* ctx, const double* xyz, int64_t n, double radius, int max_nn, int32_t* out_idx,
+                     double* out_d2, int32_t* out_cnt, void* stream);
+
+/* compute_fpfh_feature(pcd, KDTreeSearchParamHybrid(radius, max_nn))
+ * (processing.py:91-94: radius 5 voxel, max_nn 100): per point its SPFH (the
+ * pair features -- fdlibm acos / atan2 -- of its neighbours, 11 bins each,
+ * 100 / (neighbours - 1) per pair) and the FPFH = the 1/d2-weighted sum of the
+ * neighbours' SPFH, each third scaled to 100, + its own SPFH (zero for a
+ * point without neighbours) -> feature [n][33] f64 (device; Open3D's
+ * Feature.data_ transposed).  normals: [n][3] (estimate_normals).  Blocking. */
+int sl_compute_fpfh(sl_ctx* ctx, const double* xyz, const double* normals, int64_t n, double radius, int max_nn,
+                    double* feature, void* stream);
+
+/* The nearest row of b [nb][dim] for every row of a [na][dim] (device f64;
+ * dim == 33): nanoflann's L2 order (four dimensions at a time, then the
+ * rest), ties to the lower index -> out [na] (device int32).  Blocking. */
+int sl_feature_nn(sl_ctx* ctx, const double* a, int64_t na, const double* b, int64_t nb, int dim, int32_t* out,
+                  void* stream);
+
+/* registration_ransac_based_on_feature_matching(source, target, source_feature,
+ * target_feature, mutual_filter, max_distance,
+ * TransformationEstimationPointToPoint(False), 3,
+ * [CorrespondenceCheckerBasedOnEdgeLength(edge_similarity),
+ *  CorrespondenceCheckerBasedOnDistance(max_distance)],
+ * RANSACConvergenceCriteria(max_iteration, confidence)) (processing.py:98-111):
+ * correspondences = feature nearest neighbours (mutual: both ways agree; fewer
+ * than 0.1f * n_src mutual pairs: the one-way set); then Open3D's RANSAC loop
+ * as one thread runs it -- iteration i draws correspondences
+ * splitmix64(seed + (3 i + k + 1) * 0x9E3779B97F4A7C15) (k = 0..2; Open3D's
+ * std::mt19937 draw is unseeded, so no run of it is reproducible), checks edge
+ * lengths, fits Umeyama (Eigen's 3x3 JacobiSVD), checks distances, and
+ * validates (fitness = source points with a target within max_distance / n,
+ * inlier RMSE); the best by (fitness, then lower RMSE) updates the estimated
+ * iteration count log(1 - confidence) / log(1 - inlier_ratio^3) -- evaluated
+ * on the GPU in batches of hypotheses, walked in iteration order.
+ * source / target [n][3], features [n][33]: device f64.  Host outputs: the
+ * row-major 4x4 transformation (identity if nothing validated), fitness,
+ * inlier_rmse, iterations run, validations (hypotheses that passed both
+ * checkers) and the correspondence count (any output pointer but
+ * transformation may be NULL).  Blocking on `stream`. */
+int sl_ransac_feature_matching(sl_ctx* ctx, const double* source, int64_t n_src, const double* target, int64_t n_tgt,
+                               const double* source_feature, const double* target_feature, int mutual_filter,
+                               double max_distance, double edge_similarity, int max_iteration, double confidence,
+                               uint64_t seed, double* transformation, double* fitness, double* inlier_rmse,
+                               int* iterations, int* validations, int64_t* n_corres, void* stream);
 
 /* Release the scratch buffers the merge entry points keep pooled for `device`
  * (kept otherwise for the process's lifetime, at most 16 GiB per device);

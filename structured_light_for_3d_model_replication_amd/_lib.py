@@ -34,7 +34,8 @@ EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_err
            "sl_set_calib", "sl_decode_triangulate", "sl_mask_counts_to", "sl_stack_ready", "sl_stack_next", "sl_call_prepare", "sl_call_run", "sl_call_destroy", "sl_triangulate_maps", "sl_sync",
            "sl_last_thresholds", "sl_last_launch_info", "sl_profile_enable", "sl_profile_read", "sl_time_kernels", "sl_format_ply", "sl_write_ply",
            "sl_write_ply_binary", "sl_voxel_downsample", "sl_statistical_outliers", "sl_select_by_index",
-           "sl_transform_points", "sl_estimate_normals", "sl_icp_point_to_plane", "sl_merge_pool_trim", "sl_calib_products", "sl_gather_unique_id", "sl_gather_init", "sl_gather_counts",
+           "sl_transform_points", "sl_estimate_normals", "sl_icp_point_to_plane", "sl_radius_search", "sl_compute_fpfh",
+           "sl_feature_nn", "sl_ransac_feature_matching", "sl_merge_pool_trim", "sl_calib_products", "sl_gather_unique_id", "sl_gather_init", "sl_gather_counts",
            "sl_gather",
            "sl_decode_triangulate_batch", "sl_last_error")
 
@@ -79,6 +80,13 @@ _SIGS = {
     "sl_icp_point_to_plane": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, ctypes.c_double, _vp, _i32, ctypes.c_double,
                                       ctypes.c_double, _vp, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i32), _vp]),
+    "sl_radius_search": (_i32, [_vp, _vp, _i64, ctypes.c_double, _i32, _vp, _vp, _vp, _vp]),
+    "sl_compute_fpfh": (_i32, [_vp, _vp, _vp, _i64, ctypes.c_double, _i32, _vp, _vp]),
+    "sl_feature_nn": (_i32, [_vp, _vp, _i64, _vp, _i64, _i32, _vp, _vp]),
+    "sl_ransac_feature_matching": (_i32, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i32, ctypes.c_double,
+                                           ctypes.c_double, _i32, ctypes.c_double, ctypes.c_uint64, _vp,
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(_i32), ctypes.POINTER(_i32), ctypes.POINTER(_i64), _vp]),
     "sl_merge_pool_trim": (_i32, [_i32, ctypes.POINTER(_i64)]),
     "sl_gather_unique_id": (_i32, [_vp]),
     "sl_gather_init": (_i32, [_vp, _i32, _i32, _vp]),

@@ -2107,3 +2107,6 @@ int sl_merge_pool_trim(int device, int64_t* released_bytes) {
 }
 
 }  // extern "C"
+
+// global registration (FPFH, feature matching, RANSAC): the same translation unit
+#include "slreg.inl"

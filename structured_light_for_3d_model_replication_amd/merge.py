@@ -15,11 +15,13 @@ against.
 
 Registration.  The reference aligns consecutive views by FPFH + RANSAC
 (a global estimate) refined by point-to-plane ICP (:145-157) and accumulates
-the transforms (:159-167).  ``merge_pro_360`` keeps that flow with the ICP on
-the GPU (``registration_icp``: sl_icp_point_to_plane, Open3D's loop and
-point-to-plane step; parity vs Open3D unpinned, oracle/merge_oracle.py
-restates it) and the RANSAC estimate replaced by a seed: the turntable's
-relative pose between the two views (``seed_poses``), or the identity.
+the transforms (:159-167).  ``merge_pro_360`` keeps that flow on the GPU:
+``compute_fpfh_feature`` (sl_compute_fpfh), ``registration_ransac_based_on_
+feature_matching`` (sl_ransac_feature_matching) and ``registration_icp``
+(sl_icp_point_to_plane) -- Open3D's algorithms; parity vs Open3D unpinned,
+oracle/registration_oracle.py and oracle/merge_oracle.py restate them.  With
+``seed_poses`` (a turntable's known poses) the RANSAC estimate is replaced by
+the relative pose between the two views.
 ``merge_pro_360_posed`` skips registration and takes the poses as they are
 (the same ones ``Reconstructor.decode_triangulate`` applies inside k_cloud).
 """
@@ -175,6 +177,109 @@ def registration_icp(source, target, target_normals, max_correspondence_distance
             "iterations": it.value}
 
 
+def radius_search(points, radius: float, max_nn: int, *, device=None):
+    """KDTreeFlann.search_hybrid_vector_3d of every point (sl_radius_search)
+    -> (idx int32 [N, max_nn], d2 f64 [N, max_nn], count int32 [N]) on the
+    device; row i's first count[i] entries, ascending (d2, index)."""
+    eng = _engine(device)
+    P = _f64(points, eng.device)
+    n = P.shape[0]
+    idx = torch.empty((max(n, 1), max_nn), dtype=torch.int32, device=eng.device)
+    d2 = torch.empty((max(n, 1), max_nn), dtype=torch.float64, device=eng.device)
+    cnt = torch.empty(max(n, 1), dtype=torch.int32, device=eng.device)
+    with eng._lock:
+        _lib.check(eng._L.sl_radius_search(eng._ctx, _ptr(P), n, float(radius), int(max_nn), idx.data_ptr(),
+                                           d2.data_ptr(), cnt.data_ptr(), eng._stream(None)),
+                   eng._ctx, "sl_radius_search")
+    return idx[:n], d2[:n], cnt[:n]
+
+
+def compute_fpfh_feature(points, normals, radius: float, max_nn: int = 100, *, device=None) -> torch.Tensor:
+    """o3d.pipelines.registration.compute_fpfh_feature(pcd,
+    KDTreeSearchParamHybrid(radius, max_nn)) (processing.py:91-94) ->
+    features f64 [N, 33] on the device (Open3D's Feature.data transposed)."""
+    eng = _engine(device)
+    P = _f64(points, eng.device)
+    N = _f64(normals, eng.device)
+    if N.shape != P.shape:
+        raise ValueError("compute_fpfh_feature needs a normal per point")
+    n = P.shape[0]
+    out = torch.empty((max(n, 1), 33), dtype=torch.float64, device=eng.device)
+    with eng._lock:
+        _lib.check(eng._L.sl_compute_fpfh(eng._ctx, _ptr(P), _ptr(N), n, float(radius), int(max_nn), out.data_ptr(),
+                                          eng._stream(None)), eng._ctx, "sl_compute_fpfh")
+    return out[:n]
+
+
+def feature_nn(a, b, *, device=None) -> torch.Tensor:
+    """Nearest row of ``b`` for every row of ``a`` (33-D features,
+    sl_feature_nn) -> int32 [len(a)] on the device."""
+    eng = _engine(device)
+    A = torch.as_tensor(a).to(device=eng.device, dtype=torch.float64).contiguous()
+    B = torch.as_tensor(b).to(device=eng.device, dtype=torch.float64).contiguous()
+    if A.dim() != 2 or B.dim() != 2 or A.shape[1] != 33 or B.shape[1] != 33:
+        raise ValueError("features must be [N, 33]")
+    out = torch.empty(max(A.shape[0], 1), dtype=torch.int32, device=eng.device)
+    with eng._lock:
+        _lib.check(eng._L.sl_feature_nn(eng._ctx, _ptr(A), A.shape[0], _ptr(B), B.shape[0], 33, out.data_ptr(),
+                                        eng._stream(None)), eng._ctx, "sl_feature_nn")
+    return out[:A.shape[0]]
+
+
+def registration_ransac_based_on_feature_matching(source, target, source_feature, target_feature,
+                                                  mutual_filter: bool, max_correspondence_distance: float, *,
+                                                  edge_similarity: float = 0.9, max_iteration: int = 100000,
+                                                  confidence: float = 0.999, seed: int = 0, device=None) -> dict:
+    """o3d.pipelines.registration.registration_ransac_based_on_feature_matching
+    (source, target, source_fpfh, target_fpfh, mutual_filter,
+    max_correspondence_distance, TransformationEstimationPointToPoint(False),
+    3, [CorrespondenceCheckerBasedOnEdgeLength(edge_similarity),
+    CorrespondenceCheckerBasedOnDistance(max_correspondence_distance)],
+    RANSACConvergenceCriteria(max_iteration, confidence)) (processing.py:
+    98-111) on the GPU (sl_ransac_feature_matching; ``seed`` fixes the draw,
+    which Open3D leaves unseeded) -> {"transformation": 4x4 numpy, "fitness",
+    "inlier_rmse", "iterations", "validations", "correspondences"}."""
+    eng = _engine(device)
+    S = _f64(source, eng.device)
+    T = _f64(target, eng.device)
+    FS = torch.as_tensor(source_feature).to(device=eng.device, dtype=torch.float64).contiguous()
+    FT = torch.as_tensor(target_feature).to(device=eng.device, dtype=torch.float64).contiguous()
+    if FS.shape != (S.shape[0], 33) or FT.shape != (T.shape[0], 33):
+        raise ValueError("features must be [N, 33], one row per point")
+    out = np.zeros(16)
+    fit, rmse = ctypes.c_double(), ctypes.c_double()
+    it, vals, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+    with eng._lock:
+        _lib.check(eng._L.sl_ransac_feature_matching(
+            eng._ctx, _ptr(S) if len(S) else None, S.shape[0], _ptr(T) if len(T) else None, T.shape[0],
+            _ptr(FS) if len(FS) else None, _ptr(FT) if len(FT) else None, int(bool(mutual_filter)),
+            float(max_correspondence_distance), float(edge_similarity), int(max_iteration), float(confidence),
+            int(seed) & ((1 << 64) - 1), out.ctypes.data, ctypes.byref(fit), ctypes.byref(rmse), ctypes.byref(it),
+            ctypes.byref(vals), ctypes.byref(nc), eng._stream(None)), eng._ctx, "sl_ransac_feature_matching")
+    return {"transformation": out.reshape(4, 4), "fitness": fit.value, "inlier_rmse": rmse.value,
+            "iterations": it.value, "validations": vals.value, "correspondences": nc.value}
+
+
+def preprocess_point_cloud(points, voxel_size: float, *, device=None):
+    """preprocess_point_cloud (processing.py:79-96): voxel_down_sample, normals
+    (radius 2 voxel, max_nn 30), FPFH (radius 5 voxel, max_nn 100) ->
+    (down points, their normals, their features) on the device."""
+    Pd, _ = voxel_down_sample(points, None, voxel_size, device=device)
+    Nd = estimate_normals(Pd, voxel_size * 2, 30, device=device)
+    Fd = compute_fpfh_feature(Pd, Nd, voxel_size * 5, 100, device=device)
+    return Pd, Nd, Fd
+
+
+def execute_global_registration(source_down, target_down, source_fpfh, target_fpfh, voxel_size: float, *,
+                                seed: int = 0, device=None) -> dict:
+    """execute_global_registration (processing.py:98-113): RANSAC on FPFH
+    matches with the reference's settings (mutual filter, distance 1.5 voxel,
+    edge length 0.9, 100000 iterations, confidence 0.999)."""
+    return registration_ransac_based_on_feature_matching(
+        source_down, target_down, source_fpfh, target_fpfh, True, voxel_size * 1.5, edge_similarity=0.9,
+        max_iteration=100000, confidence=0.999, seed=seed, device=device)
+
+
 def rigid_inverse(M) -> np.ndarray:
     """[R | t]^-1 = [R^T | -(R^T t)] of a rigid 4x4 pose."""
     M = np.asarray(M, dtype=np.float64).reshape(4, 4)
@@ -201,7 +306,7 @@ def mat4(a, b) -> np.ndarray:
 
 def merge_pro_360(input_folder, output_path, voxel_size: float = 0.02, *, seed_poses=None, device=None,
                   binary: bool = True, order: str = "lexicographic", max_iteration: int = 30,
-                  return_transforms: bool = False):
+                  return_transforms: bool = False, ransac_seed: int = 0):
     """merge_pro_360 (processing.py:116-182): the clouds of ``input_folder``
     (``ply_files(order)``; default the reference's lexicographic order)
     registered in sequence -- scan i onto scan i-1 by point-to-plane ICP
@@ -211,12 +316,14 @@ def merge_pro_360(input_folder, output_path, voxel_size: float = 0.02, *, seed_p
     by T_i -- then merged, voxel-downsampled, outlier-filtered, normals
     estimated and written in Open3D's layout (as merge_pro_360_posed).
 
-    The reference seeds each ICP with an FPFH + RANSAC global estimate; here
-    the seed is ``inverse(seed_poses[i-1]) @ seed_poses[i]`` (the turntable's
-    relative pose between the two views; poses mapping each view into a
-    common frame, e.g. synth.turntable_pose), or the identity when
-    ``seed_poses`` is None.  Returns (points, colors, normals) on the device
-    (+ the accumulated transforms with ``return_transforms``)."""
+    Each ICP starts, as the reference's, from the FPFH + RANSAC global
+    estimate (preprocess_point_cloud / execute_global_registration, :79-113:
+    FPFH radius 5 voxel, RANSAC distance 1.5 voxel; ``ransac_seed`` fixes its
+    draw), unless ``seed_poses`` is given: then from ``inverse(seed_poses[i-1])
+    @ seed_poses[i]`` (the turntable's relative pose between the two views;
+    poses mapping each view into a common frame, e.g. synth.turntable_pose).
+    Returns (points, colors, normals) on the device (+ the accumulated
+    transforms with ``return_transforms``)."""
     print(f"[Merge 360] Loading clouds from {input_folder}...")
     files = ply_files(input_folder, order)
     if len(files) < 2:
@@ -234,19 +341,26 @@ def merge_pro_360(input_folder, output_path, voxel_size: float = 0.02, *, seed_p
     print(f"[Merge 360] Loaded {len(pcds)} clouds. Running Sequential Registration (New360 Logic)...")
     down = {}
 
-    def prep(i):  # preprocess_point_cloud (:79-96) without the FPFH features (no RANSAC)
+    def prep(i):  # preprocess_point_cloud (:79-96); the FPFH features only for RANSAC
         if i not in down:
-            Pd, _ = voxel_down_sample(pcds[i][0], None, voxel_size, device=eng.device)
-            down[i] = (Pd, estimate_normals(Pd, voxel_size * 2, 30, device=eng.device))
+            if seed_poses is None:
+                down[i] = preprocess_point_cloud(pcds[i][0], voxel_size, device=eng.device)
+            else:
+                Pd, _ = voxel_down_sample(pcds[i][0], None, voxel_size, device=eng.device)
+                down[i] = (Pd, estimate_normals(Pd, voxel_size * 2, 30, device=eng.device), None)
         return down[i]
     accum = np.eye(4)
     transforms = [accum.copy()]
     parts_p, parts_c = [pcds[0][0]], [pcds[0][1]]
     for i in range(1, len(pcds)):
         print(f"[Merge 360] Aligning Scan {i} -> Scan {i-1}...")
-        src, _ = prep(i)
-        tgt, tgt_n = prep(i - 1)
-        init = np.eye(4) if seed_poses is None else mat4(rigid_inverse(seed_poses[i - 1]), seed_poses[i])
+        src, _, src_f = prep(i)
+        tgt, tgt_n, tgt_f = prep(i - 1)
+        if seed_poses is None:  # execute_global_registration (:146-151)
+            init = execute_global_registration(src, tgt, src_f, tgt_f, voxel_size, seed=ransac_seed + i,
+                                               device=eng.device)["transformation"]
+        else:
+            init = mat4(rigid_inverse(seed_poses[i - 1]), seed_poses[i])
         T_local = registration_icp(src, tgt, tgt_n, voxel_size, init, max_iteration=max_iteration,
                                    device=eng.device)["transformation"]
         accum = mat4(accum, T_local)

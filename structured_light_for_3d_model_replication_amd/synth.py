@@ -138,11 +138,16 @@ def _sphere_hit(o, d, center, radius):
 
 def render_stack(rig: Rig, n_cols: int | None = None, n_rows: int | None = None,
                  view_deg: float = 0.0, seed: int = 0, device="cpu",
-                 include_rows: bool = True, shadow_frac_scale: float = 1.0):
+                 include_rows: bool = True, shadow_frac_scale: float = 1.0, scene: str = "default"):
     """Render one view's capture stack.
 
     Returns ``(stack uint8 [n_img,H,W], texture uint8 [H,W,3] BGR)`` on
     ``device`` with ``n_img = 2 + 2*(nc + nr)`` (nr = 0 if not include_rows).
+    ``scene``: "default" (the SURVEY §8(d) scene: a sphere with a bump in front
+    of a wall); "turntable" (no wall; two bumps fixed to the sphere, the whole
+    object turned by ``view_deg`` about the vertical axis through its centre,
+    so that turntable_pose(view_deg) maps every view back onto view 0 exactly:
+    the registration tests' rigid, asymmetric object).
     """
     dev = torch.device(device)
     g = torch.Generator(device=dev)
@@ -160,13 +165,21 @@ def render_stack(rig: Rig, n_cols: int | None = None, n_rows: int | None = None,
 
     center = torch.tensor([0.0, 0.0, 600.0], device=dev, dtype=f32)
     a = math.radians(view_deg)
-    off = torch.tensor([110.0 * math.cos(a) - 0.0, -70.0, -110.0 * math.sin(a) - 60.0],
-                       device=dev, dtype=f32)
-    bump = center + off
-    t_big = _sphere_hit(o, d, center, 150.0)
-    t_bump = _sphere_hit(o, d, bump, 45.0)
-    t_wall = torch.where(d[..., 2] > 1e-6, 900.0 / d[..., 2], torch.full_like(u, float("inf")))
-    t = torch.minimum(torch.minimum(t_big, t_bump), t_wall)
+    if scene == "turntable":
+        ca, sa = math.cos(a), math.sin(a)
+        spheres = [(center, 150.0)] + [
+            (center + torch.tensor([ox * ca + oz * sa, oy, -ox * sa + oz * ca], device=dev, dtype=f32), r_)
+            for (ox, oy, oz), r_ in (((110.0, -70.0, -60.0), 45.0), ((-60.0, 90.0, -100.0), 35.0))]
+        t = torch.full_like(u, float("inf"))
+    elif scene == "default":
+        off = torch.tensor([110.0 * math.cos(a) - 0.0, -70.0, -110.0 * math.sin(a) - 60.0],
+                           device=dev, dtype=f32)
+        spheres = [(center, 150.0), (center + off, 45.0)]
+        t = torch.where(d[..., 2] > 1e-6, 900.0 / d[..., 2], torch.full_like(u, float("inf")))  # the wall
+    else:
+        raise ValueError("scene must be 'default' or 'turntable'")
+    for c_, r_ in spheres:
+        t = torch.minimum(t, _sphere_hit(o, d, c_, r_))
     X = d * t[..., None]
 
     R = torch.tensor(rig.R, dtype=f32, device=dev)
@@ -184,7 +197,7 @@ def render_stack(rig: Rig, n_cols: int | None = None, n_rows: int | None = None,
     seg = X - Cp
     dist = seg.norm(dim=-1)
     dirp = seg / dist[..., None].clamp(min=1e-6)
-    for c_, r_ in ((center, 150.0), (bump, 45.0)):
+    for c_, r_ in spheres:
         th = _sphere_hit(Cp, dirp, c_, r_)
         lit &= ~(th < dist * (1 - 1e-3) - 0.5)
     col = torch.where(lit, col, torch.zeros_like(col)).to(torch.int64)

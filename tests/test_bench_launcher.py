@@ -45,6 +45,14 @@ def test_gpus_n_starts_n_ranks(n, scaling, views, expect):
     assert m["per_rank_points"] == m["gather_counts"] == r["counts"]
     assert m["gather_bytes_to_root"] == 15 * (expect - r["counts"][0])
     assert m["gather_ms"] > 0 and m["gather_GBps"] > 0
+    # the strong-scaled config-3 leg (36 views sharded over the N ranks)
+    sc = m["strong_c3"]
+    assert sc["comm_size"] == n and sc["views_total"] == 36
+    assert sc["per_rank_views"] == [len(range(-(-r * 36 // n), -(-(r + 1) * 36 // n))) for r in range(n)]
+    assert sum(sc["per_rank_views"]) == 36
+    assert sc["gather_counts"] == [1000 * v for v in sc["per_rank_views"]] == sc["per_rank_points"]
+    assert len(sc["per_rank_ms_per_step"]) == n and sc["ms_per_step"] == max(sc["per_rank_ms_per_step"])
+    assert sc["px_per_s"] > 0 and sc["gather_bytes_to_root"] == 15 * 1000 * (36 - sc["per_rank_views"][0])
 
 
 def test_gpus_disagreeing_with_world_size_is_an_error():
@@ -90,5 +98,6 @@ def test_bench_defaults_next_stats_and_graph():
     import bench
     a = bench.parse([])
     assert a.next_stats and a.graph and a.xyz == "exact"
-    a = bench.parse(["--no-next-stats", "--no-graph"])
-    assert not a.next_stats and not a.graph
+    assert a.verify and a.single_shot >= 20 and a.strong_leg
+    a = bench.parse(["--no-next-stats", "--no-graph", "--no-verify", "--no-strong-leg", "--single-shot", "0"])
+    assert not a.next_stats and not a.graph and not a.verify and not a.strong_leg and a.single_shot == 0

@@ -1,0 +1,77 @@
+"""The headline bench path itself, at full size, against the oracle (VERDICT
+r3 #2): BASELINE config 2 -- one 3840x2160 view, 11+11-bit column + row Gray
+code with inverses (46 planes), maps + cloud, xyz = float32 of the
+reference's f64 (sl_system.py:508-653) -- run exactly as bench.py runs it: the
+bench's own synthetic view (seed 1000*2 + 0), on a stream of its own, every
+call naming the next call's stack (sl_stack_next: the 4K pre-stats grid inside
+k_cloud), eager calls first, then K chained calls captured into a hipGraph and
+replayed once.  Every call's col/row maps, mask, point count, xyz and BGR must
+equal the oracle's (GPU only)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import sl_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(res, ref, what):
+    col, row, mask, P, C = ref
+    np.testing.assert_array_equal(res["col_map"][0].cpu().numpy(), col, err_msg=f"{what}: col_map")
+    np.testing.assert_array_equal(res["row_map"][0].cpu().numpy(), row, err_msg=f"{what}: row_map")
+    np.testing.assert_array_equal(res["mask"][0].cpu().numpy(), mask, err_msg=f"{what}: mask")
+    cloud = res["cloud"]
+    n = cloud.total()
+    assert n == len(P), f"{what}: {n} points, oracle {len(P)}"
+    np.testing.assert_array_equal(cloud.xyz[:n].cpu().numpy().view(np.uint32), P.astype(np.float32).view(np.uint32),
+                                  err_msg=f"{what}: xyz")
+    np.testing.assert_array_equal(cloud.bgr[:n].cpu().numpy(), C, err_msg=f"{what}: bgr")
+
+
+def test_headline_c2_chain_graph_full_size():
+    import bench
+    from structured_light_for_3d_model_replication_amd import core, synth
+    cfg = bench.CONFIGS["c2"]
+    H, W, Wp, Hp = cfg["H"], cfg["W"], cfg["Wp"], cfg["Hp"]
+    rig = synth.Rig(H=H, W=W, Wp=Wp, Hp=Hp)
+    st, tx = synth.render_stack(rig, seed=1000 * 2 + 0, include_rows=True, view_deg=0.0, device="cuda")
+    stack, tex = st[None].contiguous(), tx[None].contiguous()
+    cal = synth.make_calibration(rig, with_Nc=False)
+    ref = o.decode_triangulate(list(st.cpu().numpy()), tx.cpu().numpy(), cal, Wp, Hp)
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    s = torch.cuda.Stream()
+    K = 3  # a multiple of the 3-buffer pre-stats rotation: the captured chain can be replayed again
+    outs = [{} for _ in range(K)]
+
+    def call(o_):
+        return eng.decode_triangulate(stack, Wp, Hp, texture=tex, maps=True, cloud=True, xyz_dtype=torch.float32,
+                                      out=o_, next_stack=stack)
+    with torch.cuda.stream(s):
+        eager = [call(o_) for o_ in outs]  # the first one runs k_stats; the rest take the pre-stats pass
+    torch.cuda.synchronize()
+    for k, r in enumerate(eager):
+        _check(r, ref, f"eager call {k}")
+    for o_ in outs:
+        for v in o_.values():
+            v.zero_()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+        res = [call(o_) for o_ in outs]
+    with torch.cuda.stream(s):
+        g.replay()
+    torch.cuda.synchronize()
+    for k, r in enumerate(res):
+        _check(r, ref, f"graph call {k}")
+    # a second replay: with K a multiple of 3 the buffer the first captured
+    # call reads is the one the last one filled, and the one it fills was zeroed
+    for o_ in outs:
+        for v in o_.values():
+            v.zero_()
+    with torch.cuda.stream(s):
+        g.replay()
+    torch.cuda.synchronize()
+    for k, r in enumerate(res):
+        _check(r, ref, f"second replay, call {k}")
