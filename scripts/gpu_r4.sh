@@ -19,7 +19,7 @@ for spec in "$@"; do
   echo "== $kind $label [$envs] $args"
   case $kind in
     tests)
-      env $envs timeout -k 10 900 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread $args \
+      env $envs timeout -k 10 900 python -u -m pytest -m gpu -q --maxfail 25 --timeout 300 --timeout-method thread $args \
         > "$O/$label.log" 2>&1 || { tail -40 "$O/$label.log"; exit 1; }
       tail -1 "$O/$label.log" ;;
     bench)
