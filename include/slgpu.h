@@ -72,7 +72,15 @@ const char* sl_ctx_last_error(const sl_ctx* ctx);
 
 /* Pre-size the context's scratch for up to `max_views` views of `max_px`
  * pixels each so that later calls allocate nothing (required before stream
- * capture into a hipGraph).  Calls grow scratch on demand otherwise. */
+ * capture into a hipGraph).  Calls grow scratch on demand otherwise.
+ * Graphs: a context rotates part of its scratch from launch group to launch
+ * group without host work (block-sum buffers over 2, the pre-stats
+ * histograms of sl_stack_next over 3, the adaptive-mask histograms of
+ * k_stats over 2), so a captured sequence of calls replays correctly right
+ * after its capture; it replays again and again only when it holds a
+ * multiple of 6 launch groups (each rotation back at its start).  An
+ * out-of-phase replay writes no point past out_capacity (the cloud's total in
+ * view_offsets then exceeds it) but its results are invalid. */
 int sl_ctx_reserve(sl_ctx* ctx, int64_t max_views, int64_t max_px);
 
 /* Upload calibration for an H x W camera (the calib.mat fields loaded at

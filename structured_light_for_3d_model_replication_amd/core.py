@@ -53,7 +53,12 @@ class Cloud:
         return self.xyz[o[v]:o[v + 1]], self.bgr[o[v]:o[v + 1]]
 
     def total(self) -> int:
-        return int(self.view_offsets[-1].item())
+        n = int(self.view_offsets[-1].item())
+        if not 0 <= n <= self.xyz.shape[0]:
+            raise RuntimeError(f"cloud total {n} is outside the output capacity {self.xyz.shape[0]}: the "
+                               "context's scratch was out of phase with this call (e.g. a captured graph replayed "
+                               "with a launch count that is not a multiple of 6, include/slgpu.h)")
+        return n
 
 
 def calibration_arrays(calib: dict, H: int, W: int):

@@ -206,6 +206,7 @@ struct Params {
   uint8_t* mask_out;
   void* xyz;
   uint8_t* bgr;
+  int64_t out_cap;         // points xyz / bgr hold (k_cloud writes nothing past it)
   int64_t* view_offsets;
   ViewStats* stats;
   unsigned long long* masked;  // or null: += masked pixels of each view (sl_mask_counts_to; the
@@ -1639,6 +1640,11 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   const int incl = wave_incl_scan(n_l, lane);
   const int total = __shfl(incl, 63, 64);
   if (lane == 0 && civ == 0) p.view_offsets[view] = base;
+  // offsets past the caller's capacity can only come from scratch out of
+  // phase with its launches (e.g. a captured graph replayed when its launch
+  // count is not a multiple of the scratch rotations, slgpu.h): write nothing
+  // (the call's total then exceeds the capacity, which the host reports)
+  if (base < 0 || base + total > p.out_cap) return;
   if (kAblate & 8) {  // measurement only: stop after the loads and the rank scan
     if (total == -1) p.bgr[0] = static_cast<uint8_t>(d[0] ^ tq[0].x ^ tq[1].y ^ tq[2].z);
     return;
@@ -3400,6 +3406,7 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   p.mask_out = mask_out;
   p.xyz = xyz;
   p.bgr = bgr;
+  p.out_cap = cap;
   p.view_offsets = view_offsets;
   p.masked = reinterpret_cast<unsigned long long*>(masked);
   const int nc_bit = (xyz && c->d_nc) ? M_NC : 0;
@@ -3510,6 +3517,7 @@ int sl_triangulate_maps(sl_ctx* c, const int32_t* col_map, const uint8_t* mask, 
   p.poses = poses;
   p.xyz = xyz;
   p.bgr = bgr;
+  p.out_cap = cap;
   p.view_offsets = view_offsets;
   const int nc_bit = c->d_nc ? M_NC : 0;
   const int decode_mode = M_FROMMAPS | M_CODES | nc_bit;

@@ -890,20 +890,22 @@ int sl_ransac_feature_matching(sl_ctx* c, const double* source, int64_t ns, cons
   MTRY(c, hipMemcpyAsync(hij.data(), ij.p, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, s));
   if (mutual_filter) MTRY(c, hipMemcpyAsync(hji.data(), ji.p, sizeof(int32_t) * nt, hipMemcpyDeviceToHost, s));
   MTRY(c, hipStreamSynchronize(s));
+  // (a row without a nearest neighbour -- NaN features -- makes no pair)
   std::vector<int32_t> cor;
   if (mutual_filter) {
     for (int64_t i = 0; i < ns; ++i)
-      if (hji[hij[i]] == i) {
+      if (hij[i] >= 0 && hji[hij[i]] == i) {
         cor.push_back(static_cast<int32_t>(i));
         cor.push_back(hij[i]);
       }
   }
   if (!mutual_filter || static_cast<int64_t>(cor.size() / 2) < static_cast<int64_t>(0.1f * static_cast<float>(ns))) {
     cor.clear();
-    for (int64_t i = 0; i < ns; ++i) {
-      cor.push_back(static_cast<int32_t>(i));
-      cor.push_back(hij[i]);
-    }
+    for (int64_t i = 0; i < ns; ++i)
+      if (hij[i] >= 0) {
+        cor.push_back(static_cast<int32_t>(i));
+        cor.push_back(hij[i]);
+      }
   }
   nc = static_cast<int64_t>(cor.size() / 2);
   if (nc < 3 || !(max_distance > 0.0)) return finish();

@@ -42,7 +42,7 @@ def test_headline_c2_chain_graph_full_size():
     eng = core.Reconstructor(torch.device("cuda", 0))
     eng.set_calibration(cal, H, W)
     s = torch.cuda.Stream()
-    K = 3  # a multiple of the 3-buffer pre-stats rotation: the captured chain can be replayed again
+    K = 6  # a multiple of the scratch rotations (2 and 3 buffers, slgpu.h): the graph replays again and again
     outs = [{} for _ in range(K)]
 
     def call(o_):
@@ -65,11 +65,12 @@ def test_headline_c2_chain_graph_full_size():
     torch.cuda.synchronize()
     for k, r in enumerate(res):
         _check(r, ref, f"graph call {k}")
-    # a second replay: with K a multiple of 3 the buffer the first captured
-    # call reads is the one the last one filled, and the one it fills was zeroed
+    # a second replay: with K a multiple of 6 every rotating scratch buffer is
+    # back in the phase the capture started from
     for o_ in outs:
         for v in o_.values():
             v.zero_()
+    torch.cuda.synchronize()
     with torch.cuda.stream(s):
         g.replay()
     torch.cuda.synchronize()
