@@ -5,7 +5,10 @@ copies of the rendering.  scripts/traffic_from_pmc.py --per-step N then
 divides every step kernel's summed bytes by N (the first call's k_stats,
 which no earlier call computed, is 1/N of a k_stats per step).
 
-    python scripts/steps_app.py [--steps 40] [--no-next-stats]
+    python scripts/steps_app.py [--steps 40] [--no-next-stats] [--views V --cloud-only]
+
+--views V --cloud-only: the multi-view configs' kernel shape instead (V 4K
+views per call, cloud only: k_decode<11, 0, ...> and the exact k_cloud).
 """
 import argparse
 import os
@@ -19,17 +22,22 @@ from structured_light_for_3d_model_replication_amd import core, synth  # noqa: E
 ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--no-next-stats", dest="next_stats", action="store_false", default=True)
+ap.add_argument("--views", type=int, default=1)
+ap.add_argument("--cloud-only", dest="cloud_only", action="store_true")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 rig = synth.Rig(H=2160, W=3840)
 cal = synth.make_calibration(rig, with_Nc=False)
-st, tx = synth.render_stack(rig, seed=2000, device=dev)
+views = [synth.render_stack(rig, seed=2000 + v, view_deg=1.0 * v, device=dev) for v in range(a.views)]
+st = torch.stack([s_ for s_, _ in views]) if a.views > 1 else views[0][0]
+tx = torch.stack([t_ for _, t_ in views]) if a.views > 1 else views[0][1]
+del views
 eng = core.Reconstructor(dev)
 eng.set_calibration(cal, rig.H, rig.W)
 out = {}
 nxt = st if a.next_stats else None
 for _ in range(a.steps):
-    eng.decode_triangulate(st, 1920, 1080, texture=tx, maps=True, cloud=True, xyz_dtype=torch.float32, out=out,
-                           next_stack=nxt)
+    eng.decode_triangulate(st, 1920, 1080, texture=tx, maps=not a.cloud_only, cloud=True, xyz_dtype=torch.float32,
+                           out=out, next_stack=nxt)
 eng.sync()
 print(f"steps {a.steps} points {int(out['view_offsets'][-1].item())}")
