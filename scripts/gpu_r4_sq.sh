@@ -2,6 +2,7 @@
 # (5 x 4K views per launch, the c5 shape) against the microbenchmark of its
 # bare access pattern at the same scale (scripts/micro/cloud_decode_floor:
 # 24 planes + 12-bit records of 5 views, 995 MB per launch, HBM-resident),
+# and of the posed exact k_cloud beside it (the c5 call: poses on),
 # plus both kernels' timings.  -> gpurun_out/r4sq (copied to profiles/r04_sq/)
 set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -22,7 +23,7 @@ for P in "$P1" "$P2" "$P3"; do
   k=$((k+1))
   rm -rf $O/p$k $O/q$k
   timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $O/p$k -o p -- ./scripts/micro/cloud_decode_floor 5 > $O/p$k.log 2>&1 || { tail -5 $O/p$k.log; exit 1; }
-  timeout -s KILL 180 rocprofv3 --pmc $P --output-format csv -d $O/q$k -o q -- python3 -u scripts/steps_app.py --views 5 --cloud-only --steps 6 > $O/q$k.log 2>&1 || { tail -5 $O/q$k.log; exit 1; }
+  timeout -s KILL 180 rocprofv3 --pmc $P --output-format csv -d $O/q$k -o q -- python3 -u scripts/steps_app.py --views 5 --cloud-only --poses --steps 6 > $O/q$k.log 2>&1 || { tail -5 $O/q$k.log; exit 1; }
   cp $(find $O/p$k -name '*counter_collection.csv' | head -1) $O/floor_pass$k.csv
   cp $(find $O/q$k -name '*counter_collection.csv' | head -1) $O/decode_pass$k.csv
   rm -rf $O/p$k $O/q$k

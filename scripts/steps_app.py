@@ -24,6 +24,7 @@ ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--no-next-stats", dest="next_stats", action="store_false", default=True)
 ap.add_argument("--views", type=int, default=1)
 ap.add_argument("--cloud-only", dest="cloud_only", action="store_true")
+ap.add_argument("--poses", action="store_true", help="turntable poses (config 5's epilogue)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 rig = synth.Rig(H=2160, W=3840)
@@ -32,12 +33,16 @@ views = [synth.render_stack(rig, seed=2000 + v, view_deg=1.0 * v, device=dev) fo
 st = torch.stack([s_ for s_, _ in views]) if a.views > 1 else views[0][0]
 tx = torch.stack([t_ for _, t_ in views]) if a.views > 1 else views[0][1]
 del views
+poses = None
+if a.poses:
+    import numpy as np
+    poses = torch.from_numpy(np.stack([synth.turntable_pose(1.0 * v) for v in range(a.views)])).to(dev)
 eng = core.Reconstructor(dev)
 eng.set_calibration(cal, rig.H, rig.W)
 out = {}
 nxt = st if a.next_stats else None
 for _ in range(a.steps):
     eng.decode_triangulate(st, 1920, 1080, texture=tx, maps=not a.cloud_only, cloud=True, xyz_dtype=torch.float32,
-                           out=out, next_stack=nxt)
+                           out=out, next_stack=nxt, poses=poses)
 eng.sync()
 print(f"steps {a.steps} points {int(out['view_offsets'][-1].item())}")
