@@ -217,6 +217,8 @@ struct Params {
   int* chunk_counts;       // k_count -> k_cloud: points per chunk
   int* block_sums;         // k_count -> k_cloud: points per workgroup (4 chunks)
   int bs_atomic;           // k_decode M_DECIDE: block sums by the last wave to arrive (no barrier)
+  int decode_dyn;          // k_decode M_DECIDE | M_CODES: chunk groups after the first round pulled from a
+                           // per-view counter (super_sums' last entries), not strided (SLGPU_DECODE_DYN=1, A/B)
   // two-level block prefix: every block (workgroup of 4 chunks) also adds its
   // sum to super_sums[block >> sb_shift]; k_cloud's offset = the super-block
   // sums before its super-block + the block sums before it inside it
@@ -774,7 +776,14 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
   // workgroup-uniform loop holds no barrier.
   const int ngroups = (p.cpv + kWaves - 1) / kWaves;
   int mx_acc = -1024;
-  for (int cg = blockIdx.x; cg < ngroups; cg += gx) {
+  __shared__ int s_next[2];  // decode_dyn: the workgroup's next chunk group
+  const bool dyn = p.decode_dyn && decide && (mode & M_CODES) && !(mode & M_FUSED) && !p.bs_atomic;
+  unsigned* const dyn_ctr = p.super_sums + (p.super_cap - 1 - view);
+  for (int cg = blockIdx.x; cg < ngroups;) {
+  // decode_dyn: this workgroup's claim on a later chunk group, issued now so
+  // that its round trip overlaps this group's loads (published below)
+  unsigned dyn_next = 0u;
+  if (dyn && tid == 0) dyn_next = atomicAdd(dyn_ctr, 1u);
   const int civ = cg * kWaves + wid;  // chunk in view
   const bool live = civ < p.cpv;
   const int64_t px0 = static_cast<int64_t>(civ) * kChunk + lane * kPx;
@@ -1081,6 +1090,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
     }
   }
   if (decide && (mode & M_CODES) && !p.bs_atomic && !(mode & M_FUSED)) {  // the workgroup's block sum (k_count's, for k_cloud's offsets)
+    if (dyn && tid == 0) s_next[it & 1] = static_cast<int>(dyn_next) + gx;
     __syncthreads();
     if (tid == 0) {
       int t = 0;
@@ -1092,6 +1102,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
     }
   }
   if (mode & M_FUSED) group_hook(col, pt_rec, live, n_px, civ, cg, s_lds);
+  cg = dyn ? s_next[it & 1] : cg + gx;  // (dyn: published before the block-sum barrier above)
   ++it;
   }  // chunk groups
 
@@ -2430,6 +2441,8 @@ struct sl_ctx {
   int pre_mix = 0;                    // SLGPU_PRE_MIX=1: pre-stats workgroups spread among k_cloud's (A/B)
   int pre_wgs = 0;                    // SLGPU_PRE_WGS=n: pre-stats workgroups in all (A/B; 0: 8 per CU)
   bool pre_decode = false;            // SLGPU_PRE_DECODE=1: pre-stats workgroups in k_decode's tail (A/B)
+  int64_t max_chunks = kMaxChunks;    // chunks per launch group (SLGPU_GROUP_CHUNKS=n, at most kMaxChunks: A/B)
+  bool decode_dyn = false;            // SLGPU_DECODE_DYN=1: k_decode's later rounds pulled dynamically (A/B)
   bool decode_balance = false;        // SLGPU_DECODE_BALANCE=1: the capped k_decode grid shrunk so that every
                                       // workgroup decodes the same number of chunk groups (A/B)
   struct {
@@ -2654,7 +2667,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
            hipStream_t s, PreArms arms, bool ready = false, hipEvent_t ready_ev = nullptr) {
   const bool decide = (decode_mode & M_DECIDE) != 0;
   const int64_t cpv = p0.cpv;
-  const int vpg = static_cast<int>(std::max<int64_t>(1, kMaxChunks / cpv));  // views per group
+  const int vpg = static_cast<int>(std::max<int64_t>(1, c->max_chunks / cpv));  // views per group
   const int n_groups = static_cast<int>((p0.n_views + vpg - 1) / vpg);
   const bool adaptive = (decode_mode & M_HIST) != 0;
   // k_stats on the side stream (never while `s` is being captured into a
@@ -2830,6 +2843,13 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     // barrier-free block sums when every k_decode workgroup iterates at most
     // kBsSlots chunk groups (4 chunks of at most 1024 points: 16-bit sums)
     p.bs_atomic = decide && (grid.x + dgrid.x - 1) / dgrid.x <= static_cast<unsigned>(kBsSlots);
+    // SLGPU_DECODE_DYN=1 (A/B): a cloud call's capped decode grid pulls its chunk
+    // groups after the first round from per-view counters (the last entries of
+    // this launch's super-block buffer, zeroed with it); block sums then take
+    // the barrier path, whose barrier publishes each workgroup's next group
+    p.decode_dyn = (c->decode_dyn && decide && (decode_mode & M_CODES) && dgrid.x < grid.x &&
+                    ((static_cast<int64_t>(grid.x) * nv) >> p.sb_shift) + 1 + nv < kSuperCap) ? 1 : 0;
+    if (p.decode_dyn) p.bs_atomic = 0;
     c->last.grid[1] = c->last.grid[2] = grid;
     c->last.s = s;
     c->last.fn[2] = nullptr;
@@ -3116,6 +3136,9 @@ int sl_ctx_create(int device, sl_ctx** out) {
   if (const char* d = getenv("SLGPU_PRE_WGS")) c->pre_wgs = std::max(0, atoi(d));
   if (const char* d = getenv("SLGPU_PRE_DECODE")) c->pre_decode = atoi(d) != 0;
   if (const char* d = getenv("SLGPU_DECODE_BALANCE")) c->decode_balance = atoi(d) != 0;
+  if (const char* d = getenv("SLGPU_DECODE_DYN")) c->decode_dyn = atoi(d) != 0;
+  if (const char* d = getenv("SLGPU_GROUP_CHUNKS"))
+    c->max_chunks = std::max<int64_t>(1, std::min<int64_t>(kMaxChunks, atoll(d)));
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
@@ -3156,7 +3179,7 @@ const char* sl_ctx_last_error(const sl_ctx* c) { return c ? c->err.c_str() : "nu
 int sl_ctx_reserve(sl_ctx* c, int64_t max_views, int64_t max_px) {
   if (!c || max_views < 1 || max_px < 1) return fail(c, SL_EINVAL, "sl_ctx_reserve: bad sizes");
   HIP_TRY(c, hipSetDevice(c->device));
-  const int64_t vpg = std::max<int64_t>(1, kMaxChunks / ((max_px + kChunk - 1) / kChunk));
+  const int64_t vpg = std::max<int64_t>(1, c->max_chunks / ((max_px + kChunk - 1) / kChunk));
   int r = ensure_scratch(c, std::min(vpg, max_views), max_px, true);
   if (r) return r;
   return grow(c, &c->d_stats, &c->cap_stats, max_views);

@@ -387,3 +387,27 @@ def test_prepared_call_after_close_raises():
     eng.close()
     with pytest.raises(RuntimeError):
         pc.run()
+
+
+@pytest.mark.parametrize("maps", [False, True])
+def test_decode_dynamic_groups_identical(maps, monkeypatch):
+    """SLGPU_DECODE_DYN=1 (A/B switch: k_decode's chunk groups after the first
+    round pulled from per-view counters): outputs identical to the default
+    strided grid, on 1080p views whose chunk groups outnumber the capped grid,
+    chained (pre-stats) and not."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W, V = 1080, 1920, 3
+    rig, base, A, TA = _group_views(H, W, V, maps, 500)
+    cal = synth.make_calibration(rig, with_Nc=False)
+    kw = dict(texture=TA, maps=maps, cloud=True, xyz_dtype=torch.float32)
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    ref = _snap(eng.decode_triangulate(A, out={}, **kw), eng)[:-1]
+    eng.sync()
+    monkeypatch.setenv("SLGPU_DECODE_DYN", "1")
+    dyn = core.Reconstructor(torch.device("cuda", 0))
+    dyn.set_calibration(cal, H, W)
+    for k in range(3):
+        r = dyn.decode_triangulate(A, out={}, next_stack=A if k < 2 else None, **kw)
+        dyn.sync()
+        _same(_snap(r, dyn)[:-1], ref, f"dynamic call {k}")
