@@ -1456,6 +1456,10 @@ __global__ __launch_bounds__(kThreads, SLGPU_COUNT_WAVES) void k_count(Params p)
 #define SLGPU_PIPE 4
 #endif
 constexpr int kPipe = SLGPU_PIPE;  // points per lane per pass in k_cloud
+#ifndef SLGPU_POSE_COARSE
+#define SLGPU_POSE_COARSE 1
+#endif
+constexpr bool kPoseCoarse = SLGPU_POSE_COARSE != 0;  // posed verified route: the coarse bound of M_k (A/B)
 #ifndef SLGPU_SMALL_PIPE
 #define SLGPU_SMALL_PIPE 4
 #endif
@@ -1720,10 +1724,12 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
   const double* pose = p.poses ? p.poses + 16 * view : nullptr;
   // the view's pose rows, once per chunk into wave-uniform registers (read
   // through `pose` inside the point loop they were re-loaded per point)
-  double pm[12];
+  double pm[12], pr[3] = {0.0, 0.0, 0.0};
   if (pose) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) pm[k] = uniform_f64(pose[k]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pr[k] = (fabs(pm[4 * k]) + fabs(pm[4 * k + 1])) + fabs(pm[4 * k + 2]);
   }
   const bool f64out = (mode & M_XYZ64) != 0;
   constexpr int dbg = kAblate;
@@ -1929,9 +1935,21 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           const double X2 = ((pm[0] * x0 + pm[1] * x1) + pm[2] * x2) + pm[3];
           const double Y2 = ((pm[4] * x0 + pm[5] * x1) + pm[6] * x2) + pm[7];
           const double Z2 = ((pm[8] * x0 + pm[9] * x1) + pm[10] * x2) + pm[11];
-          const double M0 = ((fabs(pm[0] * x0) + fabs(pm[1] * x1)) + fabs(pm[2] * x2)) + fabs(pm[3]);
-          const double M1 = ((fabs(pm[4] * x0) + fabs(pm[5] * x1)) + fabs(pm[6] * x2)) + fabs(pm[7]);
-          const double M2 = ((fabs(pm[8] * x0) + fabs(pm[9] * x1)) + fabs(pm[10] * x2)) + fabs(pm[11]);
+          double M0, M1, M2;
+          if (kPoseCoarse) {
+            // M_k <= R_k max_j |P_j| + |m_k3| (R_k = sum_j |m_kj|, per view):
+            // a wider interval, so as safe, at 5 operations instead of 18
+            // (the slack of 2^-44 against the 2^-45.2 the bound needs covers
+            // these few roundings)
+            const double pmax = fmax(fmax(fabs(x0), fabs(x1)), fabs(x2));
+            M0 = pr[0] * pmax + fabs(pm[3]);
+            M1 = pr[1] * pmax + fabs(pm[7]);
+            M2 = pr[2] * pmax + fabs(pm[11]);
+          } else {
+            M0 = ((fabs(pm[0] * x0) + fabs(pm[1] * x1)) + fabs(pm[2] * x2)) + fabs(pm[3]);
+            M1 = ((fabs(pm[4] * x0) + fabs(pm[5] * x1)) + fabs(pm[6] * x2)) + fabs(pm[7]);
+            M2 = ((fabs(pm[8] * x0) + fabs(pm[9] * x1)) + fabs(pm[10] * x2)) + fabs(pm[11]);
+          }
           bad |= unsettled(X2, M0) | unsettled(Y2, M1) | unsettled(Z2, M2);
           X[i] = X2;
           Y[i] = Y2;
