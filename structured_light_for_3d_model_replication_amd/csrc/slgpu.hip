@@ -2460,7 +2460,8 @@ struct sl_ctx {
   int pre_wgs = 0;                    // SLGPU_PRE_WGS=n: pre-stats workgroups in all (A/B; 0: 8 per CU)
   bool pre_decode = false;            // SLGPU_PRE_DECODE=1: pre-stats workgroups in k_decode's tail (A/B)
   int64_t max_chunks = kMaxChunks;    // chunks per launch group (SLGPU_GROUP_CHUNKS=n, at most kMaxChunks: A/B)
-  bool decode_dyn = false;            // SLGPU_DECODE_DYN=1: k_decode's later rounds pulled dynamically (A/B)
+  int decode_dyn = -1;                // k_decode's later rounds pulled dynamically: -1 cloud-only calls (no
+                                      // maps), SLGPU_DECODE_DYN=0 never, =1 every cloud call (A/B)
   bool decode_balance = false;        // SLGPU_DECODE_BALANCE=1: the capped k_decode grid shrunk so that every
                                       // workgroup decodes the same number of chunk groups (A/B)
   struct {
@@ -2861,11 +2862,12 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     // barrier-free block sums when every k_decode workgroup iterates at most
     // kBsSlots chunk groups (4 chunks of at most 1024 points: 16-bit sums)
     p.bs_atomic = decide && (grid.x + dgrid.x - 1) / dgrid.x <= static_cast<unsigned>(kBsSlots);
-    // SLGPU_DECODE_DYN=1 (A/B): a cloud call's capped decode grid pulls its chunk
+    // decode_dyn (cloud-only calls; SLGPU_DECODE_DYN): a capped decode grid pulls its chunk
     // groups after the first round from per-view counters (the last entries of
     // this launch's super-block buffer, zeroed with it); block sums then take
     // the barrier path, whose barrier publishes each workgroup's next group
-    p.decode_dyn = (c->decode_dyn && decide && (decode_mode & M_CODES) && dgrid.x < grid.x &&
+    const bool dyn_want = c->decode_dyn > 0 || (c->decode_dyn < 0 && !(decode_mode & M_MAPS));
+    p.decode_dyn = (dyn_want && decide && (decode_mode & M_CODES) && dgrid.x < grid.x &&
                     ((static_cast<int64_t>(grid.x) * nv) >> p.sb_shift) + 1 + nv < kSuperCap) ? 1 : 0;
     if (p.decode_dyn) p.bs_atomic = 0;
     c->last.grid[1] = c->last.grid[2] = grid;
@@ -3154,7 +3156,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
   if (const char* d = getenv("SLGPU_PRE_WGS")) c->pre_wgs = std::max(0, atoi(d));
   if (const char* d = getenv("SLGPU_PRE_DECODE")) c->pre_decode = atoi(d) != 0;
   if (const char* d = getenv("SLGPU_DECODE_BALANCE")) c->decode_balance = atoi(d) != 0;
-  if (const char* d = getenv("SLGPU_DECODE_DYN")) c->decode_dyn = atoi(d) != 0;
+  if (const char* d = getenv("SLGPU_DECODE_DYN")) c->decode_dyn = atoi(d) != 0 ? 1 : 0;
   if (const char* d = getenv("SLGPU_GROUP_CHUNKS"))
     c->max_chunks = std::max<int64_t>(1, std::min<int64_t>(kMaxChunks, atoll(d)));
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
@@ -3672,6 +3674,28 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
       const int k = order[q];
       if (hipEventElapsedTime(&ms, ev[q], ev[q + 1]) == hipSuccess) out[k] = c->last.fn[k] ? ms / reps : 0.0;
     }
+  }
+  // a dynamic k_decode (decode_dyn) claims chunk groups from per-view counters
+  // that its launch leaves exhausted: each re-run gets fresh counters (zeroed
+  // outside its events) and is timed alone
+  if (r == SL_OK && c->last.fn[0] && c->last.p[0].decode_dyn) {
+    Params p = c->last.p[0];
+    void* args[] = {&p};
+    const unsigned nv = c->last.grid[0].y;
+    unsigned* ctr = p.super_sums + (p.super_cap - nv);
+    double sum = 0.0;
+    for (int i = 0; i < reps && r == SL_OK; ++i) {
+      float ms = 0.f;
+      if (hipMemsetAsync(ctr, 0, sizeof(unsigned) * nv, s) != hipSuccess || hipEventRecord(ev[0], s) != hipSuccess ||
+          hipLaunchKernel(c->last.fn[0], c->last.grid[0], dim3(kThreads), args, 0, s) != hipSuccess ||
+          hipEventRecord(ev[1], s) != hipSuccess || hipEventSynchronize(ev[1]) != hipSuccess ||
+          hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess) {
+        r = fail(c, SL_EHIP, "sl_time_kernels: dynamic k_decode re-run");
+        break;
+      }
+      sum += ms;
+    }
+    if (r == SL_OK) out[0] = sum / reps;
   }
   for (int k = 0; k < 4; ++k) (void)hipEventDestroy(ev[k]);
   // the re-runs accumulated into the histograms: the next calls start from zero

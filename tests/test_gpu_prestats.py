@@ -391,15 +391,17 @@ def test_prepared_call_after_close_raises():
 
 @pytest.mark.parametrize("maps", [False, True])
 def test_decode_dynamic_groups_identical(maps, monkeypatch):
-    """SLGPU_DECODE_DYN=1 (A/B switch: k_decode's chunk groups after the first
-    round pulled from per-view counters): outputs identical to the default
-    strided grid, on 1080p views whose chunk groups outnumber the capped grid,
-    chained (pre-stats) and not."""
+    """The dynamic decode grid (k_decode's chunk groups after the first round
+    pulled from per-view counters; the default for cloud-only calls,
+    SLGPU_DECODE_DYN=1 forces it on maps calls too): outputs identical to the
+    strided grid (SLGPU_DECODE_DYN=0), on 1080p views whose chunk groups
+    outnumber the capped grid, chained (pre-stats) and not."""
     from structured_light_for_3d_model_replication_amd import core, synth
     H, W, V = 1080, 1920, 3
     rig, base, A, TA = _group_views(H, W, V, maps, 500)
     cal = synth.make_calibration(rig, with_Nc=False)
     kw = dict(texture=TA, maps=maps, cloud=True, xyz_dtype=torch.float32)
+    monkeypatch.setenv("SLGPU_DECODE_DYN", "0")
     eng = core.Reconstructor(torch.device("cuda", 0))
     eng.set_calibration(cal, H, W)
     ref = _snap(eng.decode_triangulate(A, out={}, **kw), eng)[:-1]
@@ -411,3 +413,10 @@ def test_decode_dynamic_groups_identical(maps, monkeypatch):
         r = dyn.decode_triangulate(A, out={}, next_stack=A if k < 2 else None, **kw)
         dyn.sync()
         _same(_snap(r, dyn)[:-1], ref, f"dynamic call {k}")
+    # sl_time_kernels re-runs the dynamic k_decode on fresh counters: a full
+    # decode each time (an exhausted counter would leave a near-empty launch)
+    eng.decode_triangulate(A, out={}, **kw)
+    t_ref = eng.time_kernels(5)
+    dyn.decode_triangulate(A, out={}, **kw)
+    t_dyn = dyn.time_kernels(5)
+    assert t_dyn[0] > 0.6 * t_ref[0], (t_dyn, t_ref)
