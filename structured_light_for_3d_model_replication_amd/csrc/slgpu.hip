@@ -173,6 +173,11 @@ struct Params {
   const uint8_t* in_mask;
   int64_t HW;
   int H, W;
+  // px / W = (px * w_magic) >> w_shift for 0 <= px < HW: 2^w_shift > HW * W and
+  // w_magic = floor(2^w_shift / W) + 1 < 2^32 (fill_common).  k_decode's row
+  // of a pixel without the compiler's reciprocal, a loop invariant VGPR
+  uint32_t w_magic;
+  int w_shift;
   int n_views;
   int cpv;           // chunks per view
   int64_t n_chunks;  // n_views * cpv
@@ -272,6 +277,28 @@ __device__ __forceinline__ uint32_t gt_msb(uint32_t a, uint32_t b) {
   return ((a & ~b) | (~(a ^ b) & low)) & H;
 }
 
+// Bit 7 of each byte: byte k of a > byte k of b (the other bits are garbage).
+// a > b  <=>  !(b >= a); d = (b | 0x80) - (a & 0x7f) stays in [1, 255] per
+// byte (no borrow crosses bytes) and its bit 7 is (b & 0x7f) >= (a & 0x7f);
+// with the two top bits that is one three-input boolean of (a, b, d): 4
+// instructions against gt_msb's 7.  Ties give 0 (strict, sl_system.py:561).
+__device__ __forceinline__ uint32_t gt_bit7(uint32_t a, uint32_t b) {
+  const uint32_t H = 0x80808080u;
+  const uint32_t d = (b | H) - (a & ~H);
+  // ~((b & ~a) | (~(a ^ b) & d)) as one v_bitop3 (truth table over src0 = 0xf0,
+  // src1 = 0xcc, src2 = 0xaa: 0x71); the compiler's own matching splits it in 3
+  return __builtin_amdgcn_bitop3_b32(a, b, d, 0x71);
+}
+
+// Gray -> binary within each byte's low `bits`-bit field (zeros above it):
+// the prefix xor from the field's top bit down, 4 pixels per word.
+__device__ __forceinline__ uint32_t gray_to_binary_bytes(uint32_t x, int bits) {
+  if (bits > 1) x ^= (x >> 1) & 0x7f7f7f7fu;
+  if (bits > 2) x ^= (x >> 2) & 0x3f3f3f3fu;
+  if (bits > 4) x ^= (x >> 4) & 0x0f0f0f0fu;
+  return x;
+}
+
 // Gray -> binary, the prefix xor that sl_system.py:567-570 iterates to a fixed
 // point (codes are < 2^16).
 __device__ __forceinline__ uint32_t gray_to_binary(uint32_t g) {
@@ -280,6 +307,12 @@ __device__ __forceinline__ uint32_t gray_to_binary(uint32_t g) {
   g ^= g >> 4;
   g ^= g >> 8;
   return g;
+}
+
+// Row of pixel px (0 <= px < HW) of the frame: px / W by Params::w_magic (one
+// 32 x 32 -> 64-bit multiply and a shift, operands in SGPRs).
+__device__ __forceinline__ int row_of(const Params& p, int px) {
+  return static_cast<int>((static_cast<uint64_t>(static_cast<uint32_t>(px)) * p.w_magic) >> p.w_shift);
 }
 
 // Inclusive prefix sum over the 64 lanes of a wave.
@@ -371,6 +404,21 @@ __device__ __forceinline__ int wave_sum(int s) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
   return s;
+}
+
+// The same sum (every lane active) without LDS permutes or address
+// registers: an inclusive scan within each row of 16 lanes by DPP row_shr
+// 1 / 2 / 4 / 8 (lanes shifted in from outside the row read 0), then the four
+// row totals read into a scalar.  k_decode's loop uses it: the permute
+// addresses of wave_sum are loop invariants the compiler hoists and, at 168
+// VGPRs, spills.
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+  return (__builtin_amdgcn_readlane(v, 15) + __builtin_amdgcn_readlane(v, 31)) +
+         (__builtin_amdgcn_readlane(v, 47) + __builtin_amdgcn_readlane(v, 63));
 }
 
 // ------------------------------------------------------------ thresholds ----
@@ -649,6 +697,12 @@ constexpr int kDecodePerCu = SLGPU_DECODE_PER_CU;  // default k_decode grid cap,
 #ifndef SLGPU_DECODE_WAVES
 #define SLGPU_DECODE_WAVES 3
 #endif
+#ifndef SLGPU_SWAR_GRAY
+#define SLGPU_SWAR_GRAY 1
+#endif
+// Gray bits gathered MSB-first into byte lanes and converted to binary there,
+// 4 pixels per instruction (0: the per-pixel conversion; measurement build)
+constexpr bool kSwarGray = SLGPU_SWAR_GRAY != 0;
 // k_decode's body; group_hook(col, pt, live, n_px, civ, cg, s_lds) runs at
 // the end of each chunk group when the mode has M_FUSED (k_fused: the
 // group's cloud in the same launch), else nothing.
@@ -794,7 +848,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
   // M_DECIDE without yn in LDS: the row's yn first (the oldest load: waiting
   // for it never waits for this iteration's stores)
   const float ys_early = (decide && !kDecYnLds && (mode & M_CODES) && n_px > 0)
-                             ? p.yn32[static_cast<int>(px0) / p.W] : 0.0f;
+                             ? p.yn32[row_of(p, static_cast<int>(px0))] : 0.0f;
   uint32_t col[kPx];
   uint32_t pt_rec = 0xffffu;  // the lane's point bits for 12-bit records (decide path)
   if (mode & M_FROMMAPS) {
@@ -846,7 +900,28 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
     // Fold one (pattern, inverse) pair into per-byte-lane accumulators:
     // acc = (acc << 1) | bit holds at most 8 bits per byte lane, so no carry
     // crosses into the neighbouring pixel; codes of up to 16 bits use A then B.
+    // (kSwarGray: each bit enters at bit 7 of its byte lane and the lane
+    // shifts right, acc = (acc >> 1 & 0x7f..) | (bit7 & 0x80..): the first
+    // pair ends lowest, bit-reversed below; 6 instructions per word and pair)
     auto consume = [&](const uint4& P, const uint4& I, int pair) {
+      if (kSwarGray) {
+        auto ins = [](uint32_t acc, uint32_t g) { return ((acc >> 1) & 0x7f7f7f7fu) | (g & 0x80808080u); };
+        uint32_t g[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) g[w] = gt_bit7(word(P, w), word(I, w));
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          if (pair < kc) {
+            if (pair < 8) cA[w] = ins(cA[w], g[w]);
+            else cB[w] = ins(cB[w], g[w]);
+          } else if (pair - kc < 8) {
+            rA[w] = ins(rA[w], g[w]);
+          } else {
+            rB[w] = ins(rB[w], g[w]);
+          }
+        }
+        return;
+      }
       uint32_t m[4];
 #pragma unroll
       for (int w = 0; w < 4; ++w) m[w] = gt_msb(word(P, w), word(I, w)) >> 7;
@@ -914,21 +989,76 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
     const int cSh = nc - kc;
     const int rSh = nr - krr;
     uint32_t row[kPx];
+    if (kSwarGray) {
+      // A code's top min(k, 8) Gray bits are in A, the rest in B, each
+      // bit-reversed by the right-shifting accumulators: bitreverse puts them
+      // MSB-first in the low bits of each byte (pixel 4 w + e in byte 3 - e).
+      // Binary per byte lane; B's bits continue A's prefix xor, so A's binary
+      // lowest bit (the parity of its Gray bits) is xor-ed into B's top bit
+      // before B's own conversion.
+      // Codes shifted by sh = n - k bits (fewer patterns than code bits):
+      // binary(g << sh) = binary(g) << sh with its lowest bit repeated below.
+      auto to_binary = [](uint32_t (&A)[4], uint32_t (&B)[4], int k) {
+        const int kA = k < 8 ? k : 8, kB = k - kA;
 #pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      const int w = k >> 2, sft = 8 * (k & 3);
-      const uint32_t gc = (((cA[w] >> sft) & 0xffu) << cBn) | ((cB[w] >> sft) & 0xffu);
-      const uint32_t gr = (((rA[w] >> sft) & 0xffu) << rBn) | ((rB[w] >> sft) & 0xffu);
-      col[k] = gray_to_binary(gc << cSh);
-      row[k] = (mode & M_ROWS) ? gray_to_binary(gr << rSh) : 0u;
+        for (int w = 0; w < 4; ++w) {
+          A[w] = gray_to_binary_bytes(__builtin_bitreverse32(A[w]), kA);
+          // (A's parity flips B's top bit: every bit below it follows)
+          B[w] = kB > 0 ? gray_to_binary_bytes(__builtin_bitreverse32(B[w]) ^ ((A[w] & 0x01010101u) << (kB - 1)), kB)
+                        : 0u;
+        }
+      };
+      to_binary(cA, cB, kc);
+#pragma unroll
+      for (int q = 0; q < kPx; ++q) {
+        const int w = q >> 2, sft = 8 * (3 - (q & 3));
+        col[q] = (((cA[w] >> sft) & 0xffu) << cBn) | ((cB[w] >> sft) & 0xffu);
+      }
+      if (cSh > 0) {
+#pragma unroll
+        for (int q = 0; q < kPx; ++q) {
+          const uint32_t lo = col[q] & 1u;
+          col[q] = (col[q] << cSh) | ((lo << cSh) - lo);
+        }
+      }
+      // rows: only the maps store reads them -- converted there, a word at a time
+      if (mode & M_ROWS) to_binary(rA, rB, krr);
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) row[k] = 0u;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {
+        const int w = k >> 2, sft = 8 * (k & 3);
+        const uint32_t gc = (((cA[w] >> sft) & 0xffu) << cBn) | ((cB[w] >> sft) & 0xffu);
+        const uint32_t gr = (((rA[w] >> sft) & 0xffu) << rBn) | ((rB[w] >> sft) & 0xffu);
+        col[k] = gray_to_binary(gc << cSh);
+        row[k] = (mode & M_ROWS) ? gray_to_binary(gr << rSh) : 0u;
+      }
     }
+    // (kSwarGray) pixel 4 w + e's row code from the binary row words
+    auto row_code = [&](int w, int e) -> uint32_t {
+      const int sft = 8 * (3 - e);
+      uint32_t v = (((rA[w] >> sft) & 0xffu) << rBn) | ((rB[w] >> sft) & 0xffu);
+      if (rSh > 0) {
+        const uint32_t lo = v & 1u;
+        v = (v << rSh) | ((lo << rSh) - lo);
+      }
+      return v;
+    };
     if (mode & M_MAPS) {
       if (vec) {
         if (n_px == kPx) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             st_map(p.col_out + o + 4 * i, col[4 * i], col[4 * i + 1], col[4 * i + 2], col[4 * i + 3]);
-            st_map(p.row_out + o + 4 * i, row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
+            if (kSwarGray) {
+              uint32_t r4[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) r4[e] = row_code(i, e);
+              st_map(p.row_out + o + 4 * i, r4[0], r4[1], r4[2], r4[3]);
+            } else {
+              st_map(p.row_out + o + 4 * i, row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
+            }
           }
         }
       } else {
@@ -936,7 +1066,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
         for (int k = 0; k < kPx; ++k) {
           if (k < n_px) {
             p.col_out[o + k] = static_cast<int32_t>(col[k]);
-            p.row_out[o + k] = static_cast<int32_t>(row[k]);
+            p.row_out[o + k] = static_cast<int32_t>(kSwarGray ? row_code(k >> 2, k & 3) : row[k]);
           }
         }
       }
@@ -955,7 +1085,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
       for (int w = 0; w < 4; ++w) ok |= mask4(word(wq, w), word(bq, w), tw2, tc2, &mb[w]) << (4 * w);
       if (n_px != kPx) ok = 0u;  // vec: whole 16-pixel groups
       if (p.masked) {  // (uniform) the chunk's masked pixels into the workgroup's count
-        const int mc = wave_sum(__popc(ok));
+        const int mc = wave_sum_dpp(__popc(ok));
         if (lane == 0 && mc) atomicAdd(&s_mcount, static_cast<unsigned>(mc));
       }
       if ((mode & M_MAPS) && n_px == kPx)
@@ -964,7 +1094,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
       uint32_t pt = 0u;
       if ((mode & M_CODES) && ok) {
         const int px0i = static_cast<int>(px0);
-        const int v = px0i / p.W, u0 = px0i - v * p.W;  // the lane's 16 pixels share row v (W % 16 == 0)
+        const int v = row_of(p, px0i), u0 = px0i - v * p.W;  // the lane's 16 pixels share row v (W % 16 == 0)
         float4 pf[kPx];
 #pragma unroll
         for (int k = 0; k < kPx; ++k) {
@@ -1020,7 +1150,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
           const uint32_t nw = (pt & 0xfu) | ((pt & 0xf0u) << 4) | ((pt & 0xf00u) << 8) | ((pt & 0xf000u) << 12);
           *reinterpret_cast<uint32_t*>(p.ptnib + gci * kChunkNib + 4 * lane) = nw;
         }
-        const int cnt = wave_sum(__popc(pt));
+        const int cnt = wave_sum_dpp(__popc(pt));
         if (lane == 0) {
           if (live) p.chunk_counts[gci] = cnt;
           const unsigned mine = live ? static_cast<unsigned>(cnt) : 0u;
@@ -3366,6 +3496,13 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.HW = static_cast<int64_t>(H) * W;
   p.H = H;
   p.W = W;
+  {  // n / W exact for n < HW: n * W < 2^w_shift (Granlund-Montgomery, round up)
+    const uint64_t hw_w = static_cast<uint64_t>(p.HW) * static_cast<uint64_t>(W);
+    int k = 0;
+    while (k < 63 && (uint64_t{1} << k) <= hw_w) ++k;
+    p.w_shift = k;
+    p.w_magic = static_cast<uint32_t>((uint64_t{1} << k) / static_cast<uint64_t>(W) + 1);
+  }
   p.n_views = n_views;
   p.cpv = static_cast<int>((p.HW + kChunk - 1) / kChunk);
   p.n_chunks = static_cast<int64_t>(n_views) * p.cpv;
