@@ -4,6 +4,7 @@
 #   tests  pytest -m gpu with args (e.g. "tests/test_gpu_prestats.py -k multi")   -> OUT/label.log
 #   bench  python bench.py args                                                   -> OUT/lines.jsonl (+ label)
 #   prof   rocprofv3 --kernel-trace --stats of python bench.py args               -> OUT/label_kernel_stats.csv
+#   trace  rocprofv3 --kernel-trace of python bench.py args (+ trace_overlap.py) -> OUT/label_kernel_trace.csv
 #   pmc    rocprofv3 --pmc <args: counters> of scripts/steps_app.py $PMC_APP      -> OUT/label_counters.csv
 #   app    rocprofv3 --kernel-trace --stats of an arbitrary program: args         -> OUT/label_kernel_stats.csv
 #   run    any command (args), stdout to OUT/label.log
@@ -53,6 +54,14 @@ for r in csv.DictReader(open(sys.argv[1])):
         print("  %9.2f us x%6s %5.1f%% %s" % (float(r["AverageNs"]) / 1e3, r["Calls"], float(r["Percentage"]), r["Name"][:70]))
 PY
       ;;
+    trace)
+      rm -rf "$O/trace_$label"
+      env $envs timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$O/trace_$label" -o t \
+        -- python3 -u bench.py $args > "$O/$label.json" 2> "$O/$label.err" || { tail -20 "$O/$label.err"; exit 1; }
+      f=$(find "$O/trace_$label" -name '*kernel_trace.csv' | head -1)
+      cp "$f" "$O/${label}_kernel_trace.csv"
+      rm -rf "$O/trace_$label"
+      python3 scripts/trace_overlap.py "$O/${label}_kernel_trace.csv" ;;
     pmc)
       rm -rf "$O/pmc_$label"
       env $envs timeout -s KILL 120 rocprofv3 --pmc $args --output-format csv -d "$O/pmc_$label" -o p \

@@ -1854,12 +1854,19 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
   const double* pose = p.poses ? p.poses + 16 * view : nullptr;
   // the view's pose rows, once per chunk into wave-uniform registers (read
   // through `pose` inside the point loop they were re-loaded per point)
-  double pm[12], pr[3] = {0.0, 0.0, 0.0};
+  // (M_VERIFY: pb_k = 2^-44 sum_j |m_kj|, pt_k = 2^-44 |m_k3|, the settle
+  // test's interval half-width scale: exact but for subnormal results, whose
+  // absolute error <= 2^-1074 (x max|P_j| < 2^100) is nothing against the
+  // half-width >= 2^-170 a normal float32 output needs)
+  double pm[12], pb[3] = {0.0, 0.0, 0.0}, pt[3] = {0.0, 0.0, 0.0};
   if (pose) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) pm[k] = uniform_f64(pose[k]);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) pr[k] = (fabs(pm[4 * k]) + fabs(pm[4 * k + 1])) + fabs(pm[4 * k + 2]);
+    for (int k = 0; k < 3; ++k) {
+      pb[k] = 0x1p-44 * ((fabs(pm[4 * k]) + fabs(pm[4 * k + 1])) + fabs(pm[4 * k + 2]));
+      pt[k] = 0x1p-44 * fabs(pm[4 * k + 3]);
+    }
   }
   const bool f64out = (mode & M_XYZ64) != 0;
   constexpr int dbg = kAblate;
@@ -2038,9 +2045,10 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
 #pragma unroll
       for (int i = 0; i < kPipe; ++i) {
         const double x = ra[i], y = rb[i];
-        const double b0 = pl[i].x * x, b1 = pl[i].y * y;
-        const double dv = (b0 + b1) + pl[i].z;                    // n . v
-        const double S = (fabs(b0) + fabs(b1)) + fabs(pl[i].z);  // sum |n_i v_i|
+        // n . v and sum |n_i v_i| by fused multiply-adds: two roundings each,
+        // fewer than the products-then-sums the bound below allows for
+        const double dv = fma(pl[i].x, x, fma(pl[i].y, y, pl[i].z));                       // n . v
+        const double S = fma(fabs(pl[i].x), fabs(x), fma(fabs(pl[i].y), fabs(y), fabs(pl[i].z)));  // sum |n_i v_i|
         const double q = -pl[i].w * recip_nr(dv);
         X[i] = x * q;
         Y[i] = y * q;
@@ -2055,30 +2063,31 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           // point is settled when float32(v - B) == float32(v + B), B =
           // 2^-44 M_k, a normal float32 (then the reference's value, inside
           // that interval, has the same float32)
-          auto unsettled = [](double v, double m) -> unsigned {
-            const double B = m * 0x1p-44;
+          auto unsettled = [](double v, double B) -> unsigned {
             const uint32_t a = __float_as_uint(static_cast<float>(v - B));
             const uint32_t b = __float_as_uint(static_cast<float>(v + B));
             return static_cast<unsigned>(a != b) | static_cast<unsigned>(((a >> 23) & 0xffu) - 1u >= 254u);
           };
           const double x0 = X[i], x1 = Y[i], x2 = Z[i];
-          const double X2 = ((pm[0] * x0 + pm[1] * x1) + pm[2] * x2) + pm[3];
-          const double Y2 = ((pm[4] * x0 + pm[5] * x1) + pm[6] * x2) + pm[7];
-          const double Z2 = ((pm[8] * x0 + pm[9] * x1) + pm[10] * x2) + pm[11];
-          double M0, M1, M2;
+          // (by fused multiply-adds: 3 roundings per output, within the
+          // 4 u M_k the bound allows this evaluation)
+          const double X2 = fma(pm[0], x0, fma(pm[1], x1, fma(pm[2], x2, pm[3])));
+          const double Y2 = fma(pm[4], x0, fma(pm[5], x1, fma(pm[6], x2, pm[7])));
+          const double Z2 = fma(pm[8], x0, fma(pm[9], x1, fma(pm[10], x2, pm[11])));
+          double M0, M1, M2;  // 2^-44 M_k (the scale folded into pb / pt: exact)
           if (kPoseCoarse) {
             // M_k <= R_k max_j |P_j| + |m_k3| (R_k = sum_j |m_kj|, per view):
-            // a wider interval, so as safe, at 5 operations instead of 18
+            // a wider interval, so as safe, at 4 operations instead of 18
             // (the slack of 2^-44 against the 2^-45.2 the bound needs covers
             // these few roundings)
             const double pmax = fmax(fmax(fabs(x0), fabs(x1)), fabs(x2));
-            M0 = pr[0] * pmax + fabs(pm[3]);
-            M1 = pr[1] * pmax + fabs(pm[7]);
-            M2 = pr[2] * pmax + fabs(pm[11]);
+            M0 = fma(pb[0], pmax, pt[0]);
+            M1 = fma(pb[1], pmax, pt[1]);
+            M2 = fma(pb[2], pmax, pt[2]);
           } else {
-            M0 = ((fabs(pm[0] * x0) + fabs(pm[1] * x1)) + fabs(pm[2] * x2)) + fabs(pm[3]);
-            M1 = ((fabs(pm[4] * x0) + fabs(pm[5] * x1)) + fabs(pm[6] * x2)) + fabs(pm[7]);
-            M2 = ((fabs(pm[8] * x0) + fabs(pm[9] * x1)) + fabs(pm[10] * x2)) + fabs(pm[11]);
+            M0 = 0x1p-44 * (((fabs(pm[0] * x0) + fabs(pm[1] * x1)) + fabs(pm[2] * x2)) + fabs(pm[3]));
+            M1 = 0x1p-44 * (((fabs(pm[4] * x0) + fabs(pm[5] * x1)) + fabs(pm[6] * x2)) + fabs(pm[7]));
+            M2 = 0x1p-44 * (((fabs(pm[8] * x0) + fabs(pm[9] * x1)) + fabs(pm[10] * x2)) + fabs(pm[11]));
           }
           bad |= unsettled(X2, M0) | unsettled(Y2, M1) | unsettled(Z2, M2);
           X[i] = X2;
