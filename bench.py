@@ -91,9 +91,6 @@ def parse(argv=None):
                     help="CPU plumbing test of the launcher / timing / gather (no GPU, no kernels)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--chain", dest="chain", action="store_true", default=False,
-                    help="lanes (--streams > 1) in a decode chain (sl_ctx_set_chain): the calls' k_decode "
-                         "launches run one after another, each beside the other lane's k_cloud")
     ap.add_argument("--preroll-ms", dest="preroll_ms", type=float, default=300.0,
                     help="untimed back-to-back steps after the warm-up, before the timed window (ms)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
@@ -691,7 +688,7 @@ def main():
     S = max(1, a.streams if a.streams is not None else cfg.get("streams", 1))
     pool = None
     if S > 1:
-        pool = core.ReconstructorPool(dev, lanes=S, reuse_outputs=True, chain=a.chain)
+        pool = core.ReconstructorPool(dev, lanes=S, reuse_outputs=True)
         pool.set_calibration(calib, H, W)
         pool.reserve(V, H * W)
         eng, out = pool.engines[0], pool._outs[0]
@@ -974,8 +971,7 @@ def main():
                                    + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
                        "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
                        "parallelism": f"views sharded over {world} GPU(s)", "streams_per_gpu": S,
-                       "stack_ready": bool(a.stack_ready), "next_stats": bool(a.next_stats),
-                       "decode_chain": bool(a.chain and S > 1)},
+                       "stack_ready": bool(a.stack_ready), "next_stats": bool(a.next_stats)},
             "timing": {"preroll": pre,
                        "step_us": spread(step_us),
                        "step_us_note": "HIP events at every step boundary, on the step's stream; intervals "

@@ -190,21 +190,6 @@ int sl_call_prepare(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_stride
 int sl_call_run(sl_call* call, void* stream);
 void sl_call_destroy(sl_call* call);
 
-/* A decode chain over contexts (views in flight on several streams, e.g.
- * ReconstructorPool's lanes): every call of an attached context enqueues its
- * first k_decode behind the last k_decode of the chain's previous call (an
- * event wait, whatever stream that call was on) and moves the chain on to its
- * own last k_decode.  The k_decode launches of the calls thus run one after
- * another in call order, each beside the previous call's k_cloud on the other
- * stream, instead of two decodes sharing HBM and then two triangulations
- * sharing the VALUs.  Results are unchanged.  Calls of one chain must be made
- * from one host thread at a time; a chain outlives the contexts attached to
- * it (NULL detaches). */
-typedef struct sl_chain sl_chain;
-sl_chain* sl_chain_create(int device);
-void sl_chain_destroy(sl_chain* chain);
-int sl_ctx_set_chain(sl_ctx* ctx, sl_chain* chain);
-
 /* reconstruct_point_cloud on caller-supplied maps (sl_system.py:584-653).
  * col_map device int32 [n_views][H][W]; mask device uint8 [n_views][H][W]
  * (non-zero = valid); tex_bgr device [n_views][H][W][3].  Outputs as above. */

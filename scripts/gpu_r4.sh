@@ -61,9 +61,7 @@ PY
       f=$(find "$O/trace_$label" -name '*kernel_trace.csv' | head -1)
       cp "$f" "$O/${label}_kernel_trace.csv"
       rm -rf "$O/trace_$label"
-      python3 scripts/trace_overlap.py "$O/${label}_kernel_trace.csv" 10 > "$O/${label}_overlap.txt"
-      gzip -f "$O/${label}_kernel_trace.csv"
-      tail -12 "$O/${label}_overlap.txt" ;;
+      python3 scripts/trace_overlap.py "$O/${label}_kernel_trace.csv" ;;
     pmc)
       rm -rf "$O/pmc_$label"
       env $envs timeout -s KILL 120 rocprofv3 --pmc $args --output-format csv -d "$O/pmc_$label" -o p \

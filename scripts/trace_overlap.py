@@ -52,42 +52,35 @@ def intersect(a, b):
     return tot
 
 
-def report(ev, label):
-    t0 = min(x[1] for x in ev)
-    span = max(x[2] for x in ev) - t0
-    qs = {}
-    for x in ev:
-        qs[x[3]] = qs.get(x[3], 0) + 1
-    by = {}
-    for k, s, e, _, _ in ev:
-        by.setdefault(k, []).append((s, e))
-    ssum = sum(e - s for _, s, e, _, _ in ev)
-    allb = union([(x[1], x[2]) for x in ev])
-    dc = intersect(by.get("k_decode", []), by.get("k_cloud", []))
-    kinds = "  ".join(f"{k} n={len(iv)} avg={sum(e - s for s, e in iv) / len(iv):.1f}" for k, iv in sorted(by.items()))
-    print(f"{label}: span {span:.0f} us, busy {allb:.0f}, decode||cloud {dc:.0f}, sum/busy {ssum / allb:.3f}, "
-          f"queues {dict(sorted(qs.items()))}  {kinds}")
-
-
 def main():
     rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_" in r["Kernel_Name"]]
-    win = float(sys.argv[2]) if len(sys.argv) > 2 else 10.0
+    win = float(sys.argv[2]) if len(sys.argv) > 2 else 20.0
     ev = []
     for r in rows:
         n = r["Kernel_Name"]
         k = next((k for k in ("k_stats", "k_decode", "k_cloud", "k_count", "k_fused") if k in n), "other")
         ev.append((k, int(r["Start_Timestamp"]) / 1e3, int(r["End_Timestamp"]) / 1e3,
                    r.get("Queue_Id", "?"), r.get("Stream_Id", "?")))
-    ev.sort(key=lambda x: x[1])
-    # consecutive windows of `win` ms over the whole run (idle gaps > 5 ms
-    # start a new window): the timed window is the multi-queue stretch
-    cur = [ev[0]]
-    for x in ev[1:]:
-        if x[1] - cur[0][1] > win * 1e3 or x[1] - max(y[2] for y in cur[-4:]) > 5e3:
-            report(cur, f"[{(cur[0][1] - ev[0][1]) / 1e3:8.1f} ms]")
-            cur = []
-        cur.append(x)
-    report(cur, f"[{(cur[0][1] - ev[0][1]) / 1e3:8.1f} ms]")
+    end = max(x[2] for x in ev)
+    ev = [x for x in ev if x[1] >= end - win * 1e3]
+    t0 = min(x[1] for x in ev)
+    qs = {}
+    for x in ev:
+        qs[(x[3], x[4])] = qs.get((x[3], x[4]), 0) + 1
+    print("dispatches by (queue, stream):", dict(sorted(qs.items())))
+    span = end - t0
+    print(f"window {span:.1f} us, {len(ev)} dispatches")
+    by = {}
+    for k, s, e, _, _ in ev:
+        by.setdefault(k, []).append((s, e))
+    ssum = 0.0
+    for k, iv in sorted(by.items()):
+        d = sum(e - s for s, e in iv)
+        ssum += d
+        print(f"  {k:9s} n={len(iv):4d}  sum {d:9.1f} us  busy {union(iv):9.1f} us  avg {d / len(iv):8.2f} us")
+    allb = union([(x[1], x[2]) for x in ev])
+    dc = intersect(by.get("k_decode", []), by.get("k_cloud", []))
+    print(f"  busy (any kernel) {allb:.1f} us of {span:.1f}; decode||cloud {dc:.1f} us; sum/busy {ssum / allb:.3f}")
 
 
 if __name__ == "__main__":

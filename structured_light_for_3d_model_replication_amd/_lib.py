@@ -31,7 +31,7 @@ SL_XYZ_F32_FAST = 2
 
 # every symbol include/slgpu.h declares
 EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_error", "sl_ctx_reserve",
-           "sl_set_calib", "sl_decode_triangulate", "sl_mask_counts_to", "sl_stack_ready", "sl_stack_next", "sl_call_prepare", "sl_call_run", "sl_call_destroy", "sl_chain_create", "sl_chain_destroy", "sl_ctx_set_chain", "sl_triangulate_maps", "sl_sync",
+           "sl_set_calib", "sl_decode_triangulate", "sl_mask_counts_to", "sl_stack_ready", "sl_stack_next", "sl_call_prepare", "sl_call_run", "sl_call_destroy", "sl_triangulate_maps", "sl_sync",
            "sl_last_thresholds", "sl_last_launch_info", "sl_profile_enable", "sl_profile_read", "sl_time_kernels", "sl_format_ply", "sl_write_ply",
            "sl_write_ply_binary", "sl_voxel_downsample", "sl_statistical_outliers", "sl_select_by_index",
            "sl_transform_points", "sl_estimate_normals", "sl_icp_point_to_plane", "sl_radius_search", "sl_compute_fpfh",
@@ -58,9 +58,6 @@ _SIGS = {
                                _vp, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _vp, ctypes.POINTER(_vp)]),
     "sl_call_run": (_i32, [_vp, _vp]),
     "sl_call_destroy": (None, [_vp]),
-    "sl_chain_create": (_vp, [_i32]),
-    "sl_chain_destroy": (None, [_vp]),
-    "sl_ctx_set_chain": (_i32, [_vp, _vp]),
     "sl_triangulate_maps": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _i64, _vp,
                                    _vp]),
     "sl_sync": (_i32, [_vp, _vp]),

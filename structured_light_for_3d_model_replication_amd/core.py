@@ -556,23 +556,12 @@ class ReconstructorPool:
     reads them, or it synchronised after reading them) -- the lane's kernels
     would otherwise overwrite results a queued reader has not consumed."""
 
-    def __init__(self, device=None, lanes: int = 2, reuse_outputs: bool = False, chain: bool = False):
+    def __init__(self, device=None, lanes: int = 2, reuse_outputs: bool = False):
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.engines = [Reconstructor(device) for _ in range(lanes)]
         self.device = self.engines[0].device
         self.streams = [torch.cuda.Stream(self.device) for _ in range(lanes)]
-        # chain=True (sl_chain_create): the lanes' k_decode launches run one
-        # after another in call order, each beside the other lane's k_cloud
-        self._chain = None
-        if chain and lanes > 1:
-            L = self.engines[0]._L
-            ch = L.sl_chain_create(int(self.device.index or 0))
-            if not ch:
-                raise RuntimeError("sl_chain_create failed")
-            self._chain = ctypes.c_void_p(ch)
-            for e in self.engines:
-                _lib.check(L.sl_ctx_set_chain(e._ctx, self._chain), e._ctx, "sl_ctx_set_chain")
         self._outs = [{} if reuse_outputs else None for _ in range(lanes)]
         self._keys = [None] * lanes  # a lane's last output shapes (reused buffers: no allocation)
         self._plans = [None] * lanes  # a lane's prepared call and its argument key (resident inputs)
@@ -661,13 +650,5 @@ class ReconstructorPool:
             if plan is not None:
                 plan[1].close()
                 self._plans[k] = None
-        if self._chain is not None:
-            for e in self.engines:
-                if e._ctx:
-                    e._L.sl_ctx_set_chain(e._ctx, None)
         for e in self.engines:
             e.close()
-        if self._chain is not None:
-            torch.cuda.synchronize(self.device)  # the chain's event may still be waited on
-            self.engines[0]._L.sl_chain_destroy(self._chain)
-            self._chain = None

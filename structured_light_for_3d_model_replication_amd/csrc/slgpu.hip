@@ -2492,23 +2492,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_fused(Params p) {
 
 // ------------------------------------------------------------------ host ----
 
-// A decode chain (sl_chain_create): contexts attached to it run their calls'
-// k_decode launches one after another, in the order the calls are made, on
-// whatever streams: each call waits for the event of the chain's previous
-// call's last k_decode and re-records it after its own.  Two contexts on two
-// streams then alternate -- one call's k_decode runs beside the other's
-// k_cloud, the HBM-bound kernel beside the VALU-bound one -- instead of
-// drifting into step (both decoding, then both triangulating).
-struct sl_chain {
-  int device = 0;
-  hipEvent_t ev = nullptr;
-  bool used = false;  // ev recorded at least once
-};
-
 struct sl_ctx {
   int device = 0;
   std::string err;
-  sl_chain* chain = nullptr;  // sl_ctx_set_chain
   // calibration
   bool has_calib = false;
   int H = 0, W = 0, Wp = 0;
@@ -3083,14 +3069,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
         if (r) return r;
       }
       void* args[] = {&pd};
-      // a decode chain: this call's k_decode launches after the chain's
-      // previous call's (whatever its stream), and the chain moves on to ours
-      if (c->chain && g == 0 && c->chain->used) HIP_TRY(c, hipStreamWaitEvent(s, c->chain->ev, 0));
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), pgrid, dim3(kThreads), args, 0, s));
-      if (c->chain && g == n_groups - 1) {
-        HIP_TRY(c, hipEventRecord(c->chain->ev, s));
-        c->chain->used = true;
-      }
       if (pre_dec && g == n_groups - 1) c->pre_armed = true;
     }
     if (adaptive && decide && (c->hist_tracked || (side_ok && c->side_groups && g + 1 < n_groups))) {
@@ -3324,32 +3303,6 @@ int sl_ctx_create(int device, sl_ctx** out) {
     return SL_EHIP;
   }
   *out = c;
-  return SL_OK;
-}
-
-sl_chain* sl_chain_create(int device) {
-  if (hipSetDevice(device) != hipSuccess) return nullptr;
-  sl_chain* ch = new (std::nothrow) sl_chain;
-  if (!ch) return nullptr;
-  ch->device = device;
-  if (hipEventCreateWithFlags(&ch->ev, hipEventDisableTiming) != hipSuccess) {
-    delete ch;
-    return nullptr;
-  }
-  return ch;
-}
-
-void sl_chain_destroy(sl_chain* ch) {
-  if (!ch) return;
-  (void)hipSetDevice(ch->device);
-  (void)hipEventDestroy(ch->ev);
-  delete ch;
-}
-
-int sl_ctx_set_chain(sl_ctx* c, sl_chain* ch) {
-  if (!c) return SL_EINVAL;
-  if (ch && ch->device != c->device) return fail(c, SL_EINVAL, "sl_ctx_set_chain: the chain is on another device");
-  c->chain = ch;
   return SL_OK;
 }
 
