@@ -65,8 +65,9 @@ __global__ __launch_bounds__(256, 3) void floor_k(const uint8_t* st, int64_t HW,
 }
 
 int main(int argc, char** argv) {
+  // cloud_decode_floor [views [H W [quick]]]: 5 views of 3840x2160 by default
   const int V = argc > 1 ? atoi(argv[1]) : 5;
-  const int64_t HW = 3840LL * 2160;
+  const int64_t HW = argc > 3 ? static_cast<int64_t>(atoi(argv[2])) * atoi(argv[3]) : 3840LL * 2160;
   const int64_t vs = kPlanesStack * HW;
   uint8_t *st, *rec;
   if (hipMalloc(&st, vs * V) != hipSuccess || hipMalloc(&rec, HW * 3 / 2 * V + 64) != hipSuccess) return 1;
@@ -77,9 +78,11 @@ int main(int argc, char** argv) {
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   const int ngroups = static_cast<int>((HW / kChunk + 3) / 4);
+  const bool quick = argc > 4;  // cloud_decode_floor V H W quick: 3 per CU, no records / k_decode's stores only
   for (int per_cu : {3, 4}) {
+    if (quick && per_cu != 3) continue;
     const int gx = (per_cu * n_cu + V - 1) / V;
-    for (int store = 0; store < 6; ++store) {
+    for (int store = 0; store < (quick ? 2 : 6); ++store) {
       float best = 1e30f, sum = 0.f;
       for (int r = 0; r < 23; ++r) {
         (void)hipEventRecord(a, 0);
@@ -95,9 +98,9 @@ int main(int argc, char** argv) {
       }
       const double bytes = (24.0 * HW + (store ? 1.5 * HW : 0.0)) * V;  // (the same 1.5 B/px in every shape)
       const double avg = sum / 20.0;
-      printf("{\"views\": %d, \"wg_per_cu\": %d, \"store_shape\": %d, \"best_us\": %.2f, \"avg_us\": %.2f, "
+      printf("{\"views\": %d, \"px_per_view\": %lld, \"wg_per_cu\": %d, \"store_shape\": %d, \"best_us\": %.2f, \"avg_us\": %.2f, "
              "\"GBps_avg\": %.0f, \"frac_avg\": %.3f}\n",
-             V, per_cu, store, best * 1e3, avg * 1e3, bytes / (avg * 1e-3) / 1e9, bytes / (avg * 1e-3) / 8e12);
+             V, static_cast<long long>(HW), per_cu, store, best * 1e3, avg * 1e3, bytes / (avg * 1e-3) / 1e9, bytes / (avg * 1e-3) / 8e12);
       fflush(stdout);
     }
   }
