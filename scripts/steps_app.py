@@ -5,7 +5,7 @@ copies of the rendering.  scripts/traffic_from_pmc.py --per-step N then
 divides every step kernel's summed bytes by N (the first call's k_stats,
 which no earlier call computed, is 1/N of a k_stats per step).
 
-    python scripts/steps_app.py [--steps 40] [--no-next-stats] [--views V --cloud-only]
+    python scripts/steps_app.py [--steps 40] [--no-next-stats] [--views V --cloud-only] [--config c3|c4|c5]
 
 --views V --cloud-only: the multi-view configs' kernel shape instead (V 4K
 views per call, cloud only: k_decode<11, 0, ...> and the exact k_cloud).
@@ -25,18 +25,24 @@ ap.add_argument("--no-next-stats", dest="next_stats", action="store_false", defa
 ap.add_argument("--views", type=int, default=1)
 ap.add_argument("--cloud-only", dest="cloud_only", action="store_true")
 ap.add_argument("--poses", action="store_true", help="turntable poses (config 5's epilogue)")
+ap.add_argument("--config", default=None,
+                help="c3 / c4 / c5: that bench config's call (frame, views, cloud only, pose) instead")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
-rig = synth.Rig(H=2160, W=3840)
+H, W, deg = 2160, 3840, 1.0
+if a.config:  # bench.py CONFIGS: one call = the config's views of one GPU
+    H, W, a.views, deg = {"c3": (1080, 1920, 36, 10.0), "c4": (3000, 4000, 45, 1.0), "c5": (2160, 3840, 45, 1.0)}[a.config]
+    a.cloud_only, a.poses = True, a.config == "c5"
+rig = synth.Rig(H=H, W=W)
 cal = synth.make_calibration(rig, with_Nc=False)
-views = [synth.render_stack(rig, seed=2000 + v, view_deg=1.0 * v, device=dev) for v in range(a.views)]
+views = [synth.render_stack(rig, seed=2000 + v, view_deg=deg * v, device=dev) for v in range(a.views)]
 st = torch.stack([s_ for s_, _ in views]) if a.views > 1 else views[0][0]
 tx = torch.stack([t_ for _, t_ in views]) if a.views > 1 else views[0][1]
 del views
 poses = None
 if a.poses:
     import numpy as np
-    poses = torch.from_numpy(np.stack([synth.turntable_pose(1.0 * v) for v in range(a.views)])).to(dev)
+    poses = torch.from_numpy(np.stack([synth.turntable_pose(deg * v) for v in range(a.views)])).to(dev)
 eng = core.Reconstructor(dev)
 eng.set_calibration(cal, rig.H, rig.W)
 out = {}
