@@ -138,9 +138,9 @@ def parse(argv=None):
                     help="N > 1: also time BASELINE config 3 strong-scaled (36 views sharded over the N ranks) "
                          "and report it in multi_gpu.strong_c3 (default)")
     ap.add_argument("--no-strong-leg", dest="strong_leg", action="store_false")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "r03_traffic_c2.json"),
+    ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
-                         "scripts/traffic_from_pmc.py)")
+                         "scripts/traffic_from_pmc.py); default profiles/r04_traffic/traffic_<config>.json")
     return ap.parse_args(argv)
 
 
@@ -942,13 +942,17 @@ def main():
         # PMC bytes (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md)
         # of the same command, from a committed profile -- not measured here
         traffic = traffic_k = None
+        if a.traffic is None:
+            a.traffic = os.path.join(REPO, "profiles", "r04_traffic", f"traffic_{a.config}.json")
         if os.path.exists(a.traffic):
             try:
                 tj = json.load(open(a.traffic))
                 if tj.get("config") == a.config and tj.get("views") == V and tj.get("decide", False) == decide \
                         and tj.get("xyz") == ("fast" if head_fast else "exact"):
                     traffic = tj.get("bytes_per_step")
-                    traffic_k = tj.get("kernels", {}).get("k_decode")
+                    traffic_k = tj.get("kernels", {}).get("k_decode")  # per step: all its launches
+                    if traffic_k is not None:
+                        traffic_k *= v_roof / V  # per launch, as achieved / algorithmic_bytes_per_launch
             except (OSError, ValueError):
                 traffic = traffic_k = None
         slots = ("k_decode", "k_stats", "k_cloud") if decide else ("k_decode", "k_count", "k_cloud")

@@ -5,7 +5,7 @@
 #   2. scripts/steps_app.py --config cN (N chained calls of the config's views,
 #      next-stats on) under the same two passes;
 #   3. scripts/traffic_from_pmc.py --calib --per-step N -> traffic_cN.json.
-#   bash scripts/gpu_r4_traffic.sh OUT c3:10 c4:3 c5:4      (config:steps ...)
+#   bash scripts/gpu_r4_traffic.sh OUT c2:40 c3:10 c4:3 c5:4      (config:steps ...)
 set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -18,9 +18,11 @@ for spec in "$@"; do
   cfg="${spec%%:*}"
   n="${spec#*:}"
   echo "== $cfg ($n calls)"
-  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$cfg -o fetch -- python3 -u scripts/steps_app.py --config $cfg --steps $n > $O/fetch_$cfg.log 2>&1 || { tail -5 $O/fetch_$cfg.log; exit 1; }
-  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_$cfg -o write -- python3 -u scripts/steps_app.py --config $cfg --steps $n > $O/write_$cfg.log 2>&1 || { tail -5 $O/write_$cfg.log; exit 1; }
-  views=$(python3 -c "print({'c3': 36, 'c4': 45, 'c5': 45}['$cfg'])")
+  sel="--config $cfg"
+  [ "$cfg" = c2 ] && sel=""   # steps_app's default: config 2's chained 4K maps + cloud steps
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$cfg -o fetch -- python3 -u scripts/steps_app.py $sel --steps $n > $O/fetch_$cfg.log 2>&1 || { tail -5 $O/fetch_$cfg.log; exit 1; }
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_$cfg -o write -- python3 -u scripts/steps_app.py $sel --steps $n > $O/write_$cfg.log 2>&1 || { tail -5 $O/write_$cfg.log; exit 1; }
+  views=$(python3 -c "print({'c2': 1, 'c3': 36, 'c4': 45, 'c5': 45}['$cfg'])")
   python3 scripts/traffic_from_pmc.py $O/fetch_$cfg $O/write_$cfg $cfg $views exact 1 $O/traffic_$cfg.json --calib $O/cal_f $O/cal_w $O/cal.json --per-step $n > /dev/null || exit 1
   python3 -c "
 import json
