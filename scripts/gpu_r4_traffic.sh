@@ -1,5 +1,5 @@
 # Round 4: calibrated HBM bytes per step of the multi-view configs' calls
-# (VERDICT r3 #1 "calibrated PMC per config"), as gpu_r3_traffic.sh does for c2:
+# (VERDICT r3 #1 "calibrated PMC per config"; round 3 had archive/gpu_r3_traffic.sh for c2):
 #   1. scripts/micro/store_calib under --pmc WRITE_SIZE and --pmc FETCH_SIZE
 #      (separate passes): the counters' factors for the kernels' access shapes;
 #   2. scripts/steps_app.py --config cN (N chained calls of the config's views,
