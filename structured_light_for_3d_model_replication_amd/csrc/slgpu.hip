@@ -139,7 +139,8 @@ constexpr int kHistStride = kHistRep + 1;  // bin stride: replica r of bin b sit
 // the LDS compaction, 32 = k_count with the fixed thresholds, 64 = k_count
 // without the |n.r| test, 128 = k_count without plane gathers, 1024 = exact k_cloud gathers
 // its planes from a 32-entry table (cache footprint), 4096 = exact k_cloud without any point
-// arithmetic.
+// arithmetic, 8192 = k_cloud without its block prefix (each chunk writes at 1024 x its index),
+// 16384 / 32768 = the exact k_cloud without its colour / xyz stores.
 #ifndef SLGPU_ABLATE
 #define SLGPU_ABLATE 0
 #endif
@@ -1608,6 +1609,17 @@ constexpr int kBgrMode = SLGPU_LDS_BGR;
 constexpr bool kLdsBgr = kBgrMode == 1;
 constexpr bool kTexLds = kBgrMode == 2;
 constexpr int kBgrWords = kLdsBgr ? kChunk : kTexLds ? 3 * kChunk / 4 + 4 : 4;  // u32 per wave
+#ifndef SLGPU_COL_DWORD
+#define SLGPU_COL_DWORD 0
+#endif
+// (measurement build, SLGPU_COL_DWORD=1: k_cloud's colour bytes staged per
+// pass in LDS, 3 per point shifted to the pass's alignment in the output,
+// then stored 8 bytes per lane.  The byte / short stores of 3-byte colours
+// cost 4x the xyz stores per byte -- kbench, 8 4K views: 46 of 262 us for 157
+// MB of colours, 75 us for 629 MB of xyz -- but the stage costs more: k_cloud
+// 262 -> 328 us, c2 30.4 -> 46.3 us; bit-exact, 204 GPU tests)
+constexpr bool kColDword = SLGPU_COL_DWORD != 0;
+constexpr int kColStage = 64 * 4 * 3 + 16;  // bytes per wave: up to 4 x 64 points + alignment
 
 
 // base + a 32-bit byte offset: the form global loads / stores take with an
@@ -1759,11 +1771,11 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
 template <int MODE, int VEC, int PIPE>
 __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
                                              int total, const uint32_t* s_ent, const uint32_t* s_bgr,
-                                             float* s_sxyz, uint8_t* s_scol);
+                                             float* s_sxyz, uint8_t* s_scol, bool col_stage);
 
 template <int MODE, int VEC, int PIPE>
 __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane, const ChunkIn& in,
-                                            uint32_t* s_ent, uint32_t* s_bgr, float* s_sxyz, uint8_t* s_scol) {
+                                            uint32_t* s_ent, uint32_t* s_bgr, float* s_sxyz, uint8_t* s_scol, bool col_stage = false) {
   const int view = static_cast<int>(gc / p.cpv);
   const int civ = static_cast<int>(gc - static_cast<int64_t>(view) * p.cpv);
   const int64_t cpx = static_cast<int64_t>(civ) * kChunk;  // chunk's first pixel
@@ -1830,7 +1842,7 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   __builtin_amdgcn_wave_barrier();
   if (kAblate & 16) return;  // measurement only: stop after the LDS compaction
 
-  cloud_points<MODE, VEC, PIPE>(p, view, cpx, base, lane, total, s_ent, s_bgr, s_sxyz, s_scol);
+  cloud_points<MODE, VEC, PIPE>(p, view, cpx, base, lane, total, s_ent, s_bgr, s_sxyz, s_scol, col_stage);
 }
 
 // Phase 3 of a chunk: its `total` compacted points (s_ent: pixel | code << 10
@@ -1839,7 +1851,7 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
 template <int MODE, int VEC, int PIPE>
 __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
                                              int total, const uint32_t* s_ent, const uint32_t* s_bgr,
-                                             float* s_sxyz, uint8_t* s_scol) {
+                                             float* s_sxyz, uint8_t* s_scol, bool col_stage) {
   constexpr int kPipe = PIPE;  // points per lane per pass
   const int mode = MODE >= 0 ? MODE : p.mode;
   const int64_t HW = p.HW;
@@ -2248,6 +2260,10 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       }
       continue;
     }
+    // (col_stage: the colours through the wave's LDS stage, shifted by the
+    // pass's first output byte modulo 8, then 8 bytes per lane)
+    const bool cst = col_stage && !(kAblate & 16384);
+    const int csh = static_cast<int>((3 * (base + j0)) & 7);
 #pragma unroll
     for (int i = 0; i < kPipe; ++i) {
       const int j = j0 + 64 * i + lane;
@@ -2258,17 +2274,58 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           xyz[0] = X[i];
           xyz[1] = Y[i];
           xyz[2] = Z[i];
+        } else if (kAblate & 32768) {  // measurement only: no xyz stores (kept live)
+          if (X[i] == -1234.5 && Y[i] == Z[i]) p.bgr[0] = 1;
         } else {
           float* xyz = at_bytes(wx, 12u * o);
           xyz[0] = static_cast<float>(X[i]);
           xyz[1] = static_cast<float>(Y[i]);
           xyz[2] = static_cast<float>(Z[i]);
         }
+        if (kAblate & 16384) {  // measurement only: no colour stores (kept live)
+          if (bgr[i] == 0x12345678u) p.bgr[1] = 1;
+          continue;
+        }
+        if (cst) {
+          uint8_t* sc = s_scol + csh + 3 * (64 * i + lane);
+          sc[0] = static_cast<uint8_t>(bgr[i]);
+          sc[1] = static_cast<uint8_t>(bgr[i] >> 8);
+          sc[2] = static_cast<uint8_t>(bgr[i] >> 16);
+          continue;
+        }
         uint8_t* cc = at_bytes(wc, 3u * o);
         cc[0] = static_cast<uint8_t>(bgr[i]);
         cc[1] = static_cast<uint8_t>(bgr[i] >> 8);
         cc[2] = static_cast<uint8_t>(bgr[i] >> 16);
       }
+    }
+    if (cst) {
+      // the pass's colour bytes [A, A + 3n), A = 3 (base + j0), from the stage
+      // (byte k of the stage = output byte A - csh + k) to the 8-byte aligned
+      // words that cover them: whole words by one 8-byte store; the first and
+      // last (shared with the neighbouring passes / chunks) byte by byte
+      __builtin_amdgcn_wave_barrier();
+      const int nbytes = csh + 3 * min(64 * kPipe, total - j0);
+      // a buffer descriptor of the pass's 8-byte aligned output (SGPRs, per
+      // pass) + the lane's 32-bit offset: no 64-bit VGPR address stays live
+      // across passes (one did, and spilled)
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          p.bgr + (3 * (base + j0) - csh), 0, nbytes, 0x00020000);
+#pragma unroll
+      for (int q0 = 0; q0 < (3 * 64 * kPipe + 7 + 7) / 8; q0 += 64) {
+        const int b0 = 8 * (q0 + lane);
+        if (b0 < nbytes) {
+          if (b0 >= csh && b0 + 8 <= nbytes) {
+            const uint2 w = *reinterpret_cast<const uint2*>(s_scol + b0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, w), rs, b0, 0, 0);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (b0 + k >= csh && b0 + k < nbytes) __builtin_amdgcn_raw_buffer_store_b8(s_scol[b0 + k], rs, b0 + k, 0, 0);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // (the next pass rewrites the stage)
     }
   }
 }
@@ -2334,7 +2391,7 @@ __global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : SLGPU_CLOUD_WAVES) voi
   __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
   __shared__ __attribute__((aligned(16))) uint32_t s_bgr[kWaves][kBgrWords];  // colours (kBgrMode)
   __shared__ float s_sxyz[kWaves][kStageOut ? 192 : 1];      // output stage: 64 points' xyz
-  __shared__ uint8_t s_scol[kWaves][kStageOut ? 192 : 4];    // and their colour bytes
+  __shared__ __attribute__((aligned(16))) uint8_t s_scol[kWaves][kStageOut ? 192 : kColDword ? kColStage : 4];  // colour bytes
   __shared__ long long s_wred[kWaves];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -2367,15 +2424,21 @@ __global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : SLGPU_CLOUD_WAVES) voi
   ChunkIn in;
   if (kCloudHoist && civ < p.cpv) cloud_load<VEC>(p, gc, lane, &in);
   const int before = (lane < wid && civ < p.cpv) ? p.chunk_counts[gc - wid + lane] : 0;  // earlier waves' chunks
-  long long base = block_offset(p, b, tid, lane, wid, s_wred);
-  base += p.base_in ? *p.base_in : 0ll;
-  base += wave_sum(before);
+  long long base;
+  if (kAblate & 8192) {  // measurement only: no block prefix (disjoint slots of 1024 points)
+    base = static_cast<long long>(gc) * kChunk;
+  } else {
+    base = block_offset(p, b, tid, lane, wid, s_wred);
+    base += p.base_in ? *p.base_in : 0ll;
+    base += wave_sum(before);
+  }
   base = uniform64(base);
   if (civ >= p.cpv) return;
   if (!kCloudHoist) cloud_load<VEC>(p, gc, lane, &in);
   if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1)
     p.view_offsets[p.n_views] = base + p.chunk_counts[gc];
-  cloud_chunk<MODE, VEC, PIPE>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0]);
+  cloud_chunk<MODE, VEC, PIPE>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0],
+                               kColDword && !kStageOut);
 }
 
 // ================================================================= k_fused ====
