@@ -1619,6 +1619,17 @@ constexpr int kBgrWords = kLdsBgr ? kChunk : kTexLds ? 3 * kChunk / 4 + 4 : 4;  
 // MB of colours, 75 us for 629 MB of xyz -- but the stage costs more: k_cloud
 // 262 -> 328 us, c2 30.4 -> 46.3 us; bit-exact, 204 GPU tests)
 constexpr bool kColDword = SLGPU_COL_DWORD != 0;
+#ifndef SLGPU_COL_OVERLAP
+#define SLGPU_COL_OVERLAP 0
+#endif
+// (measurement build, SLGPU_COL_OVERLAP=1: k_cloud's colours as one 4-byte
+// store per point at its 3-byte slot, an unaligned buffer store whose 4th
+// byte is the next point's first colour byte -- taken from the next lane by
+// DPP, so both lanes writing that byte write the same value; the chunk's last
+// point writes its 3 bytes alone.  One store instruction per 64 points instead
+// of two, bit-exact (204 GPU tests), but slower: k_cloud 261.7 -> 264.0 us
+// for 8 4K views, c2 step 120.6 -> 122.3-123.6 us)
+constexpr bool kColOverlap = SLGPU_COL_OVERLAP != 0;
 constexpr int kColStage = 64 * 4 * 3 + 16;  // bytes per wave: up to 4 x 64 points + alignment
 
 
@@ -1867,17 +1878,23 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
   // the view's pose rows, once per chunk into wave-uniform registers (read
   // through `pose` inside the point loop they were re-loaded per point)
   // (M_VERIFY: pb_k = 2^-44 sum_j |m_kj|, pt_k = 2^-44 |m_k3|, the settle
-  // test's interval half-width scale: exact but for subnormal results, whose
-  // absolute error <= 2^-1074 (x max|P_j| < 2^100) is nothing against the
-  // half-width >= 2^-170 a normal float32 output needs)
+  // test's interval half-width scale, by exponent arithmetic on the uniform
+  // bits (scalar registers, none of the 12 VGPRs a VALU product would hold):
+  // exact, or 2^-999 where the product would be tinier -- a wider interval)
+  auto scale_2m44 = [](double v) -> double {  // v >= 0, wave-uniform
+    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+    const unsigned e = static_cast<unsigned>(b >> 52) & 0x7ffu;
+    // (e <= 67: v < 2^-955, so 2^-44 v < 2^-999, the value returned)
+    return __longlong_as_double(static_cast<long long>(e > 67u ? b - (44ull << 52) : (24ull << 52)));
+  };
   double pm[12], pb[3] = {0.0, 0.0, 0.0}, pt[3] = {0.0, 0.0, 0.0};
   if (pose) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) pm[k] = uniform_f64(pose[k]);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      pb[k] = 0x1p-44 * ((fabs(pm[4 * k]) + fabs(pm[4 * k + 1])) + fabs(pm[4 * k + 2]));
-      pt[k] = 0x1p-44 * fabs(pm[4 * k + 3]);
+      pb[k] = scale_2m44(uniform_f64((fabs(pm[4 * k]) + fabs(pm[4 * k + 1])) + fabs(pm[4 * k + 2])));
+      pt[k] = scale_2m44(uniform_f64(fabs(pm[4 * k + 3])));
     }
   }
   const bool f64out = (mode & M_XYZ64) != 0;
@@ -1900,6 +1917,9 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
   };
   float* const wx = static_cast<float*>(p.xyz) + 3 * base;  // the chunk's first point (wave-uniform)
   uint8_t* const wc = p.bgr + 3 * base;
+  // (kColOverlap) the chunk's colour bytes [3 base, 3 (base + total)) as a
+  // buffer: SGPR base, 32-bit lane offsets, nothing written past its end
+  const __amdgpu_buffer_rsrc_t rs_col = __builtin_amdgcn_make_buffer_rsrc(wc, 0, 3 * total, 0x00020000);
   for (int j0 = 0; j0 < total; j0 += 64 * kPipe) {
     if (mode & M_FAST32) {
       // SL_XYZ_F32_FAST (Oc = 0, pinhole rays, no pose; host-checked): the
@@ -2284,6 +2304,19 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         }
         if (kAblate & 16384) {  // measurement only: no colour stores (kept live)
           if (bgr[i] == 0x12345678u) p.bgr[1] = 1;
+          continue;
+        }
+        if (kColOverlap && !cst) {
+          // the next point's colour: lane + 1 of this slot, or lane 0 of the next
+          const uint32_t nx = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(bgr[i]), 0x130, 0xf, 0xf, false));
+          const uint32_t nn = (i + 1 < kPipe) ? static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(bgr[i + 1 < kPipe ? i + 1 : i]))) : 0u;
+          const uint32_t next = lane == 63 ? nn : nx;
+          if (j + 1 < total && (lane < 63 || i + 1 < kPipe)) {
+            __builtin_amdgcn_raw_buffer_store_b32((bgr[i] & 0xffffffu) | (next << 24), rs_col, 3 * static_cast<int>(o), 0, 0);
+          } else {  // the chunk's last point (or a pass's last lane with no next slot): 3 bytes
+            __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(bgr[i]), rs_col, 3 * static_cast<int>(o), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<unsigned char>(bgr[i] >> 16), rs_col, 3 * static_cast<int>(o) + 2, 0, 0);
+          }
           continue;
         }
         if (cst) {
