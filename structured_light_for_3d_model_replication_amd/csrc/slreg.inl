@@ -535,18 +535,21 @@ __global__ __launch_bounds__(64) void k_fpfh(const double* spfh, int64_t n, cons
 // LDS tiles of 64 rows; one query per thread.
 constexpr int kFnTile = 64;
 constexpr int kFeatDim = 33;
-__global__ __launch_bounds__(kT) void k_feature_nn(const double* A, int64_t na, const double* B, int64_t nb,
-                                                   int32_t* out) {
-  __shared__ double s_b[kFnTile * kFeatDim];
+// Nearest row of B (L2 over 33 dims, nanoflann's accumulation order: four
+// squared differences summed per group, the groups added in turn, then the
+// last dimension; ties keep the lower index) for each row i of A, over the
+// rows [lo, hi) of B; -> (distance, index) of the best (index -1: none).
+__device__ __forceinline__ void feature_nn_range(const double* A, int64_t na, const double* B, int64_t lo,
+                                                 int64_t hi, double* s_b, double* best_out, int64_t* bi_out) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   double a[kFeatDim];
 #pragma unroll
   for (int d = 0; d < kFeatDim; ++d) a[d] = i < na ? A[kFeatDim * i + d] : 0.0;
   double best = INFINITY;
   int64_t bi = -1;
-  for (int64_t t0 = 0; t0 < nb; t0 += kFnTile) {
+  for (int64_t t0 = lo; t0 < hi; t0 += kFnTile) {
     __syncthreads();
-    const int rows = static_cast<int>(min<int64_t>(kFnTile, nb - t0));
+    const int rows = static_cast<int>(min<int64_t>(kFnTile, hi - t0));
     for (int k = threadIdx.x; k < rows * kFeatDim; k += kT) s_b[k] = B[kFeatDim * t0 + k];
     __syncthreads();
     if (i < na) {
@@ -568,7 +571,77 @@ __global__ __launch_bounds__(kT) void k_feature_nn(const double* A, int64_t na, 
       }
     }
   }
+  *best_out = best;
+  *bi_out = bi;
+}
+
+__global__ __launch_bounds__(kT) void k_feature_nn(const double* A, int64_t na, const double* B, int64_t nb,
+                                                   int32_t* out) {
+  __shared__ double s_b[kFnTile * kFeatDim];
+  double best;
+  int64_t bi;
+  feature_nn_range(A, na, B, 0, nb, s_b, &best, &bi);
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
   if (i < na) out[i] = static_cast<int32_t>(bi);
+}
+
+// The same over B split into gridDim.y ranges of `per` rows (one query block
+// per CU was a twentieth of the chip), each range's best to (pd, pi)[y][i]...
+__global__ __launch_bounds__(kT) void k_feature_nn_part(const double* A, int64_t na, const double* B, int64_t nb,
+                                                        int64_t per, double* pd, int32_t* pi) {
+  __shared__ double s_b[kFnTile * kFeatDim];
+  const int64_t lo = static_cast<int64_t>(blockIdx.y) * per;
+  double best;
+  int64_t bi;
+  feature_nn_range(A, na, B, lo, min<int64_t>(nb, lo + per), s_b, &best, &bi);
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i < na) {
+    pd[blockIdx.y * na + i] = best;
+    pi[blockIdx.y * na + i] = static_cast<int32_t>(bi);
+  }
+}
+
+// ... then folded in range order: a strictly smaller distance wins, so ties
+// keep the lower index, as the one sequential scan does.
+__global__ __launch_bounds__(kT) void k_feature_nn_fold(const double* pd, const int32_t* pi, int64_t na, int S,
+                                                        int32_t* out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kT + threadIdx.x;
+  if (i >= na) return;
+  double best = INFINITY;
+  int32_t bi = -1;
+  for (int y = 0; y < S; ++y) {
+    const double d = pd[y * na + i];
+    if (d < best) {
+      best = d;
+      bi = pi[y * na + i];
+    }
+  }
+  out[i] = bi;
+}
+
+// Launch: B split so that the grid has ~2048 workgroups (ranges of whole
+// 64-row tiles); scratch from the context's pool.
+int feature_nn_run(sl_ctx* c, const double* a, int64_t na, const double* b, int64_t nb, int32_t* out,
+                   hipStream_t s) {
+  const int64_t qb = blocks(na);
+  const int64_t tiles = (nb + kFnTile - 1) / kFnTile;
+  int64_t S = std::min<int64_t>(256, std::max<int64_t>(1, std::min<int64_t>((2048 + qb - 1) / qb, tiles)));
+  if (S <= 1) {
+    hipLaunchKernelGGL(k_feature_nn, dim3(qb), dim3(kT), 0, s, a, na, b, nb, out);
+    MTRY(c, hipGetLastError());
+    return SL_OK;
+  }
+  const int64_t per = (tiles + S - 1) / S * kFnTile;
+  S = (nb + per - 1) / per;
+  DBuf<double> pd;
+  DBuf<int32_t> pi;
+  MTRY(c, pd.alloc(S * na));
+  MTRY(c, pi.alloc(S * na));
+  hipLaunchKernelGGL(k_feature_nn_part, dim3(qb, S), dim3(kT), 0, s, a, na, b, nb, per, pd.p, pi.p);
+  hipLaunchKernelGGL(k_feature_nn_fold, dim3(qb), dim3(kT), 0, s, pd.p, pi.p, na, static_cast<int>(S), out);
+  MTRY(c, hipGetLastError());
+  MTRY(c, hipStreamSynchronize(s));  // (before the scratch goes back to the pool)
+  return SL_OK;
 }
 
 // ---- RANSAC ----
@@ -843,9 +916,10 @@ int sl_feature_nn(sl_ctx* c, const double* a, int64_t na, const double* b, int64
   if (na >= (1ll << 31) || nb >= (1ll << 31)) return slgpu_fail(c, SL_EINVAL, "at most 2^31 - 1 rows");
   if (na == 0) return SL_OK;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  PoolStream pool_stream(s);
   MTRY(c, hipSetDevice(slgpu_device(c)));
-  hipLaunchKernelGGL(k_feature_nn, dim3(blocks(na)), dim3(kT), 0, s, a, na, b, nb, out);
-  MTRY(c, hipGetLastError());
+  const int r = feature_nn_run(c, a, na, b, nb, out, s);
+  if (r) return r;
   MTRY(c, hipStreamSynchronize(s));
   return SL_OK;
 }
@@ -882,10 +956,11 @@ int sl_ransac_feature_matching(sl_ctx* c, const double* source, int64_t ns, cons
   DBuf<int32_t> ij, ji, dcor;
   MTRY(c, ij.alloc(ns));
   MTRY(c, ji.alloc(nt));
-  hipLaunchKernelGGL(k_feature_nn, dim3(blocks(ns)), dim3(kT), 0, s, source_feature, ns, target_feature, nt, ij.p);
-  if (mutual_filter)
-    hipLaunchKernelGGL(k_feature_nn, dim3(blocks(nt)), dim3(kT), 0, s, target_feature, nt, source_feature, ns, ji.p);
-  MTRY(c, hipGetLastError());
+  {
+    int r0 = feature_nn_run(c, source_feature, ns, target_feature, nt, ij.p, s);
+    if (!r0 && mutual_filter) r0 = feature_nn_run(c, target_feature, nt, source_feature, ns, ji.p, s);
+    if (r0) return r0;
+  }
   std::vector<int32_t> hij(static_cast<size_t>(ns)), hji(static_cast<size_t>(mutual_filter ? nt : 0));
   MTRY(c, hipMemcpyAsync(hij.data(), ij.p, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, s));
   if (mutual_filter) MTRY(c, hipMemcpyAsync(hji.data(), ji.p, sizeof(int32_t) * nt, hipMemcpyDeviceToHost, s));
