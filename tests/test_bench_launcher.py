@@ -101,3 +101,19 @@ def test_bench_defaults_next_stats_and_graph():
     assert a.verify and a.single_shot >= 20 and a.strong_leg
     a = bench.parse(["--no-next-stats", "--no-graph", "--no-verify", "--no-strong-leg", "--single-shot", "0"])
     assert not a.next_stats and not a.graph and not a.verify and not a.strong_leg and a.single_shot == 0
+
+
+def test_committed_traffic_profiles_match_the_configs():
+    """bench.py attaches profiles/r04_traffic/traffic_<config>.json to a line
+    only when the profile's workload is the line's (config, views per GPU,
+    decide path, exact xyz): every config of the bench but c1 has one that
+    matches, with calibrated per-kernel bytes that add up."""
+    sys.path.insert(0, REPO)
+    import bench
+    for name in ("c2", "c3", "c4", "c5"):
+        path = os.path.join(REPO, "profiles", "r04_traffic", f"traffic_{name}.json")
+        tj = json.load(open(path))
+        assert tj["config"] == name and tj["views"] == bench.CONFIGS[name]["views"], name
+        assert tj["decide"] is True and tj["xyz"] == "exact" and tj["calibration"], name
+        assert abs(sum(tj["kernels"].values()) - tj["bytes_per_step"]) <= 1e-6 * tj["bytes_per_step"], name
+        assert "k_decode" in tj["kernels"] and "k_cloud" in tj["kernels"], name
