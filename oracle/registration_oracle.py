@@ -261,24 +261,31 @@ def feature_dist2(a, B):
 
 
 def feature_nn(A, B):
-    """Nearest row of B (ties: lower index) for every row of A."""
+    """Nearest row of B (ties: lower index) for every row of A; -1 where no
+    distance is below +inf.  A NaN distance never wins, as in nanoflann's
+    search, whose candidates must compare `dist < worst` (np.argmin would
+    return the first NaN)."""
     A = np.asarray(A, dtype=np.float64)
     B = np.asarray(B, dtype=np.float64)
     out = np.empty(len(A), dtype=np.int64)
     for i in range(len(A)):
         d = feature_dist2(A[i], B)
-        out[i] = int(np.argmin(d))  # argmin: first of equal minima
+        d = np.where(np.isnan(d), np.inf, d)
+        k = int(np.argmin(d)) if len(d) else -1  # argmin: first of equal minima
+        out[i] = k if k >= 0 and d[k] < np.inf else -1
     return out
 
 
 def correspondences_from_features(fs, ft, mutual_filter=True, mutual_consistent_ratio=0.1):
-    """CorrespondencesFromFeatures -> int64 (K, 2) (source, target)."""
+    """CorrespondencesFromFeatures -> int64 (K, 2) (source, target); a row
+    without a nearest neighbour (NaN features) makes no pair."""
     ij = feature_nn(fs, ft)
-    c0 = np.stack([np.arange(len(fs)), ij], axis=1)
+    has = ij >= 0
+    c0 = np.stack([np.arange(len(fs))[has], ij[has]], axis=1)
     if not mutual_filter:
         return c0
     ji = feature_nn(ft, fs)
-    keep = ji[ij] == np.arange(len(fs))
+    keep = ji[c0[:, 1]] == c0[:, 0]
     mutual = c0[keep]
     if len(mutual) >= int(np.float32(mutual_consistent_ratio) * np.float32(len(fs))):
         return mutual

@@ -957,6 +957,9 @@ int sl_ransac_feature_matching(sl_ctx* c, const double* source, int64_t ns, cons
   MTRY(c, ij.alloc(ns));
   MTRY(c, ji.alloc(nt));
   {
+    // (both directions in one pass over the pairs -- d(a, b) and d(b, a) are
+    // the same bits -- with a wave reduction per target row for the column
+    // bests measured no faster: RANSAC 8.55 vs 8.6 ms, 12.7 vs 12.6 ms)
     int r0 = feature_nn_run(c, source_feature, ns, target_feature, nt, ij.p, s);
     if (!r0 && mutual_filter) r0 = feature_nn_run(c, target_feature, nt, source_feature, ns, ji.p, s);
     if (r0) return r0;

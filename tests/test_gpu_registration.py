@@ -149,3 +149,23 @@ def test_merge_pro_360_pose_free_recovers_turntable(mg, tmp_path):
         ang = math.degrees(math.acos(min(1.0, (np.trace(d[:3, :3]) - 1.0) / 2.0)))
         assert ang < 1.0, f"view {i}: {ang:.3f} deg off"
         assert np.linalg.norm(d[:3, 3]) < 2.0, f"view {i}: {d[:3, 3]} mm off"
+
+
+def test_mutual_matching_ties_and_nan_rows(mg):
+    """The mutual filter's two directions (one pass over the pairs on the GPU)
+    against the oracle's two scans: duplicated feature rows on both sides
+    (ties to the lower index, in each direction), NaN rows (never a match),
+    and a set just above / below the 0.1 mutual-pair fallback -- the
+    correspondence counts of short RANSAC runs equal the oracle's."""
+    rng = np.random.default_rng(11)
+    P = blob(600, seed=12)
+    Q = P + np.array([1.0, -2.0, 0.5])
+    A = rng.integers(0, 4, size=(600, 33)).astype(np.float64)  # few distinct values: many exact ties
+    B = np.concatenate([A[300:], A[:300]])
+    B[5:9] = B[4]
+    A[17] = np.nan
+    B[40] = np.nan
+    for a_f, b_f in ((A, B), (A, rng.normal(size=(600, 33)))):
+        got = mg.registration_ransac_based_on_feature_matching(P, Q, a_f, b_f, True, 1.0, max_iteration=5, seed=3)
+        want = ro.correspondences_from_features(a_f, b_f, True)
+        assert got["correspondences"] == len(want)
