@@ -342,7 +342,9 @@ int sl_compute_fpfh(sl_ctx* ctx, const double* xyz, const double* normals, int64
 
 /* The nearest row of b [nb][dim] for every row of a [na][dim] (device f64;
  * dim == 33): nanoflann's L2 order (four dimensions at a time, then the
- * rest), ties to the lower index -> out [na] (device int32).  Blocking. */
+ * rest), ties to the lower index -> out [na] (device int32); -1 for a row with
+ * no distance below +inf (NaN features never match, as nanoflann's strict
+ * compare).  Blocking. */
 int sl_feature_nn(sl_ctx* ctx, const double* a, int64_t na, const double* b, int64_t nb, int dim, int32_t* out,
                   void* stream);
 
@@ -353,7 +355,8 @@ int sl_feature_nn(sl_ctx* ctx, const double* a, int64_t na, const double* b, int
  *  CorrespondenceCheckerBasedOnDistance(max_distance)],
  * RANSACConvergenceCriteria(max_iteration, confidence)) (processing.py:98-111):
  * correspondences = feature nearest neighbours (mutual: both ways agree; fewer
- * than 0.1f * n_src mutual pairs: the one-way set); then Open3D's RANSAC loop
+ * than 0.1f * n_src mutual pairs: the one-way set; a source row without a
+ * neighbour makes no pair); then Open3D's RANSAC loop
  * as one thread runs it -- iteration i draws correspondences
  * splitmix64(seed + (3 i + k + 1) * 0x9E3779B97F4A7C15) (k = 0..2; Open3D's
  * std::mt19937 draw is unseeded, so no run of it is reproducible), checks edge
