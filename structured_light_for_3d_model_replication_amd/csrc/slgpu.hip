@@ -100,6 +100,12 @@ __device__ __forceinline__ uint32_t ld_side4(const void* p) {
   return *reinterpret_cast<const uint32_t*>(p);
 }
 typedef int v4i __attribute__((ext_vector_type(4)));
+#ifndef SLGPU_MAP_AUX
+#define SLGPU_MAP_AUX 0
+#endif
+// (measurement builds) k_decode's col / row / mask map stores as buffer stores
+// with this cache policy (16: sc1, write-through); 0: plain global stores
+constexpr int kMapAux = SLGPU_MAP_AUX;
 // 16-byte store of 4 map words at p (16-byte aligned)
 __device__ __forceinline__ void st_map(int32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   const v4i v = {static_cast<int>(a), static_cast<int>(b), static_cast<int>(c), static_cast<int>(d)};
@@ -154,6 +160,19 @@ constexpr int kMaxWp = 32768;              // projector columns (record codes ar
 #define SLGPU_MAX_CHUNKS (1 << 16)
 #endif
 constexpr int64_t kMaxChunks = SLGPU_MAX_CHUNKS;  // chunks per launch group: bounds k_cloud's prefix reads
+#ifndef SLGPU_REC_BLK
+#define SLGPU_REC_BLK 1
+#endif
+// 12-bit records in chunk slots (1536 B: a lane's 16 codes as 16 B at 16 lane
+// + 8 B at 1024 + 8 lane), the launch group's views interleaved by chunk group
+// (rec_slot), stored write-through (kRecAux = sc1).  0: pixel order, 24 B per
+// lane as two 12-B stores (A/B; scripts/micro/write_mix.hip prices both shapes)
+constexpr bool kRecBlk = SLGPU_REC_BLK != 0;
+#ifndef SLGPU_REC_AUX
+#define SLGPU_REC_AUX 16
+#endif
+constexpr int kRecAux = SLGPU_REC_AUX;
+constexpr int kRecSlot = 1536;
 
 struct ViewStats {
   int thr_white;        // mask: white > thr_white
@@ -206,6 +225,7 @@ struct Params {
   int rec12;               // decide path (Wp < 4096): records packed 12 bits per pixel, 24 B per 16
                            // pixels, code 0xfff = no point (1.5 B/px written, no point nibbles)
                            // map and k_decode writes no records (2 B/px less k_decode write traffic)
+  int rec_blk;             // rec12 records in kRecBlk's chunk slots (k_decode without maps; else pixel order)
   uint8_t* ptnib;    // [chunk][4 steps][64 lanes] point nibbles: bit e of byte (s, l) = pixel 256 s + 4 l + e
   int32_t* col_out;
   int32_t* row_out;
@@ -250,6 +270,14 @@ struct Params {
 };
 
 // ---------------------------------------------------------------- helpers ----
+
+// kRecBlk: the 1536-B record slot of chunk civ of view `view` in its launch
+// group -- chunk groups (4 chunks, one workgroup iteration) of all the group's
+// views interleaved, so that the views' workgroups, progressing together, write
+// one contiguous window of the buffer at a time
+__device__ __forceinline__ int64_t rec_slot(const Params& p, int view, int civ) {
+  return (static_cast<int64_t>(civ >> 2) * p.n_views + view) * 4 + (civ & 3);
+}
 
 __device__ __forceinline__ uint4 ld16(const uint8_t* p, int n, bool vec) {
   if (vec) return *reinterpret_cast<const uint4*>(p);
@@ -1048,7 +1076,21 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
     };
     if (mode & M_MAPS) {
       if (vec) {
-        if (n_px == kPx) {
+        if (n_px == kPx && kMapAux) {
+          const int64_t vb = view * HW;  // (4 HW < 2^31: measurement builds only)
+          const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.col_out + vb, 0, static_cast<int>(4 * HW), 0x00020000);
+          const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(p.row_out + vb, 0, static_cast<int>(4 * HW), 0x00020000);
+          const int bo = 4 * static_cast<int>(px0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            __builtin_amdgcn_raw_buffer_store_b128(v4u{col[4 * i], col[4 * i + 1], col[4 * i + 2], col[4 * i + 3]}, rc,
+                                                   bo + 16 * i, 0, kMapAux);
+            uint32_t r4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) r4[e] = kSwarGray ? row_code(i, e) : row[4 * i + e];
+            __builtin_amdgcn_raw_buffer_store_b128(v4u{r4[0], r4[1], r4[2], r4[3]}, rr, bo + 16 * i, 0, kMapAux);
+          }
+        } else if (n_px == kPx) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             st_map(p.col_out + o + 4 * i, col[4 * i], col[4 * i + 1], col[4 * i + 2], col[4 * i + 3]);
@@ -1089,8 +1131,15 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
         const int mc = wave_sum_dpp(__popc(ok));
         if (lane == 0 && mc) atomicAdd(&s_mcount, static_cast<unsigned>(mc));
       }
-      if ((mode & M_MAPS) && n_px == kPx)
-        *reinterpret_cast<uint4*>(p.mask_out + o) = make_uint4(mb[0], mb[1], mb[2], mb[3]);
+      if ((mode & M_MAPS) && n_px == kPx) {
+        if (kMapAux) {
+          const __amdgpu_buffer_rsrc_t rm =
+              __builtin_amdgcn_make_buffer_rsrc(p.mask_out + view * HW, 0, static_cast<int>(HW), 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(v4u{mb[0], mb[1], mb[2], mb[3]}, rm, static_cast<int>(px0), 0, kMapAux);
+        } else {
+          *reinterpret_cast<uint4*>(p.mask_out + o) = make_uint4(mb[0], mb[1], mb[2], mb[3]);
+        }
+      }
       // ---- |n.r| > 1e-6 (sl_system.py:638-642) of the masked pixels, LDS tables ----
       uint32_t pt = 0u;
       if ((mode & M_CODES) && ok) {
@@ -1194,8 +1243,12 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
       rec[i] = min(col[2 * i], static_cast<uint32_t>(p.Wp - 1)) |
                (min(col[2 * i + 1], static_cast<uint32_t>(p.Wp - 1)) << 16);
     if (vec && p.rec12) {
-      if (n_px == kPx) {  // 8 codes per 3 words, two 12-byte stores
-        uint32_t* ro = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p.codes) + 3 * o / 2);
+      // (chunk slots without maps: the maps kernels keep the pixel order, whose
+      // registers fit; the host sets p.rec_blk to match, for k_cloud)
+      const bool blk = kRecBlk && !(mode & M_MAPS);
+      if (n_px == kPx) {  // 8 codes per 3 words
+        uint32_t rw[6];
+        uint32_t* ro = blk ? rw : reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p.codes) + 3 * o / 2);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const uint32_t* r = rec + 4 * h;  // codes 8 h .. 8 h + 7, two per word; 0xfff: no point
@@ -1206,6 +1259,12 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
           ro[3 * h] = c0 | (c1 << 12) | (c2 << 24);  // 4-byte aligned: one dwordx3 store
           ro[3 * h + 1] = (c2 >> 8) | (c3 << 4) | (c4 << 16) | (c5 << 28);
           ro[3 * h + 2] = (c5 >> 4) | (c6 << 8) | (c7 << 20);
+        }
+        if (blk) {  // the chunk's 1536-B slot (rec_slot): words 0-3 at 16 lane, 4-5 at 1024 + 8 lane
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+              reinterpret_cast<uint8_t*>(p.codes) + kRecSlot * rec_slot(p, view, civ), 0, kRecSlot, 0x00020000);
+          __builtin_amdgcn_raw_buffer_store_b128(v4u{rw[0], rw[1], rw[2], rw[3]}, rs, 16 * lane, 0, kRecAux);
+          __builtin_amdgcn_raw_buffer_store_b64(v2u{rw[4], rw[5]}, rs, 1024 + 8 * lane, 0, kRecAux);
         }
       }
     } else if (vec) {
@@ -1710,14 +1769,21 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
     for (int i = 0; i < kPx / 2; ++i) d[i] = min(c[2 * i], cmax) | (min(c[2 * i + 1], cmax) << 16);
   } else if (vec && p.rec12) {  // 12-bit records (k_decode): 8 codes per 3 words
     in->ptbits = 0u;
-    const uint2* src = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p.codes) +
-                                                      3 * (view * HW + pxl) / 2);  // 24 B, 8-byte aligned
     uint32_t w[6];
+    if (p.rec_blk) {  // the chunk's slot: words 0-3 at 16 lane, 4-5 at 1024 + 8 lane
+      const uint8_t* cb = reinterpret_cast<const uint8_t*>(p.codes) + kRecSlot * rec_slot(p, view, civ);
+      const uint4 a = ld_side16(cb + 16 * lane);
+      const uint2 b = ld_side8(cb + 1024 + 8 * lane);
+      w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y;
+    } else {
+      const uint2* src = reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(p.codes) +
+                                                        3 * (view * HW + pxl) / 2);  // 24 B, 8-byte aligned
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const uint2 q = ld_side8(src + i);
-      w[2 * i] = q.x;
-      w[2 * i + 1] = q.y;
+      for (int i = 0; i < 3; ++i) {
+        const uint2 q = ld_side8(src + i);
+        w[2 * i] = q.x;
+        w[2 * i + 1] = q.y;
+      }
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -2819,7 +2885,10 @@ int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes) {
     if (r) return r;
     if (c->cap_hist[b] != before) c->hist_dirty[b] = 0;  // fresh (zeroed) allocation
   }
-  if (codes) return grow(c, &c->d_codes, &c->cap_codes, views * px + 16);
+  // (u16 units: 2 B/px, or kRecBlk's 1536-B slots of whole chunk groups)
+  if (codes)
+    return grow(c, &c->d_codes, &c->cap_codes,
+                std::max<int64_t>(views * px, views * ((px + 4 * kChunk - 1) / (4 * kChunk)) * 4 * (kRecSlot / 2)) + 16);
   return SL_OK;
 }
 
@@ -3039,6 +3108,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     // maps + cloud on the decide path: k_cloud reads the col map (no records)
     p.rec_col = (decide && p.col_out && cloud_mode >= 0 && c->rec_from_maps) ? p.col_out : nullptr;
     p.rec12 = (decide && vec && !p.rec_col && cloud_mode >= 0 && p.Wp < 4096 && c->rec12) ? 1 : 0;
+    p.rec_blk = (p.rec12 && kRecBlk && !(decode_mode & M_MAPS)) ? 1 : 0;  // (k_decode's `blk`)
     p.ptnib = c->d_ptnib;
     p.chunk_counts = c->d_chunk_counts;
     p.block_sums = c->d_block_sums;
