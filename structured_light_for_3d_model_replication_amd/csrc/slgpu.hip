@@ -168,6 +168,9 @@ constexpr int64_t kMaxChunks = SLGPU_MAX_CHUNKS;  // chunks per launch group: bo
 // (rec_slot), stored write-through (kRecAux = sc1).  0: pixel order, 24 B per
 // lane as two 12-B stores (A/B; scripts/micro/write_mix.hip prices both shapes)
 constexpr bool kRecBlk = SLGPU_REC_BLK != 0;
+#ifndef SLGPU_REC_BLK_MAPS
+#define SLGPU_REC_BLK_MAPS 0  // (A/B) chunk slots in the maps kernels too
+#endif
 #ifndef SLGPU_REC_AUX
 #define SLGPU_REC_AUX 16
 #endif
@@ -1245,7 +1248,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
     if (vec && p.rec12) {
       // (chunk slots without maps: the maps kernels keep the pixel order, whose
       // registers fit; the host sets p.rec_blk to match, for k_cloud)
-      const bool blk = kRecBlk && !(mode & M_MAPS);
+      const bool blk = kRecBlk && (!(mode & M_MAPS) || SLGPU_REC_BLK_MAPS);
       if (n_px == kPx) {  // 8 codes per 3 words
         uint32_t rw[6];
         uint32_t* ro = blk ? rw : reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p.codes) + 3 * o / 2);
@@ -3108,7 +3111,7 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     // maps + cloud on the decide path: k_cloud reads the col map (no records)
     p.rec_col = (decide && p.col_out && cloud_mode >= 0 && c->rec_from_maps) ? p.col_out : nullptr;
     p.rec12 = (decide && vec && !p.rec_col && cloud_mode >= 0 && p.Wp < 4096 && c->rec12) ? 1 : 0;
-    p.rec_blk = (p.rec12 && kRecBlk && !(decode_mode & M_MAPS)) ? 1 : 0;  // (k_decode's `blk`)
+    p.rec_blk = (p.rec12 && kRecBlk && (!(decode_mode & M_MAPS) || SLGPU_REC_BLK_MAPS)) ? 1 : 0;  // (k_decode's `blk`)
     p.ptnib = c->d_ptnib;
     p.chunk_counts = c->d_chunk_counts;
     p.block_sums = c->d_block_sums;
