@@ -26,6 +26,9 @@
 //     group (offset of (group, view): (group V + view) 6 KB), so that the
 //     workgroups of every view write one contiguous window at a time
 //  16 1's stores with 15's layout
+//  17-20 15 with the plane loads as buffer loads of cache policy 0 (default),
+//     2 (nt, as k_decode), 16 (sc1), 1 (sc0)
+//  21-22 reads only, buffer loads of policy 0 / 2
 // One JSON line per variant: avg / best over 20 timed launches.
 //   write_mix [views [H W]]
 #include <hip/hip_runtime.h>
@@ -53,6 +56,14 @@ __device__ __forceinline__ void words_of(const v4u (&v)[kNpl], uint32_t (&w)[6])
     b += v[p + 1];
   }
   w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = b.x; w[4] = b.y; w[5] = b.w ^ a.w;
+}
+
+template <int AUX>
+__device__ __forceinline__ void load_chunk_buf(v4u (&v)[kNpl], const uint8_t* vb, int64_t HW, int64_t px) {
+  // (a view's 24 planes span < 2 GiB: one descriptor, plane offsets in soffset)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(vb), 0, static_cast<int>(kNpl * HW), 0x00020000);
+#pragma unroll
+  for (int p = 0; p < kNpl; ++p) v[p] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(px), p * static_cast<int>(HW), AUX);
 }
 
 template <int MODE>
@@ -104,10 +115,14 @@ __global__ __launch_bounds__(256, 3) void mix_k(const uint8_t* st, int64_t HW, i
     const int64_t px = chunk * kChunk + lane * 16;
     if (px >= HW) continue;
     v4u v[kNpl];
-    load_chunk(v, vb, HW, px);
+    if (MODE == 17 || MODE == 21) load_chunk_buf<0>(v, vb, HW, px);
+    else if (MODE == 18 || MODE == 22) load_chunk_buf<2>(v, vb, HW, px);
+    else if (MODE == 19) load_chunk_buf<16>(v, vb, HW, px);
+    else if (MODE == 20) load_chunk_buf<1>(v, vb, HW, px);
+    else load_chunk(v, vb, HW, px);
     uint32_t w[6];
     words_of(v, w);
-    uint8_t* cb = (MODE == 15 || MODE == 16)
+    uint8_t* cb = (MODE == 15 || MODE == 16 || (MODE >= 17 && MODE <= 20))
                       ? rec + ((static_cast<int64_t>(cg) * gridDim.y + view) * 4 + wid) * (kChunk * 3 / 2)
                       : rb + chunk * (kChunk * 3 / 2);
     if (MODE == 1 || MODE == 6 || MODE == 16) {
@@ -120,7 +135,7 @@ __global__ __launch_bounds__(256, 3) void mix_k(const uint8_t* st, int64_t HW, i
                                                  wid * 1536 + 24 * lane);
       *reinterpret_cast<v3u*>(ro) = v3u{w[0], w[1], w[2]};
       *reinterpret_cast<v3u*>(ro + 3) = v3u{w[3], w[4], w[5]};
-    } else if (MODE == 3 || MODE == 4 || MODE == 15) {
+    } else if (MODE == 3 || MODE == 4 || MODE == 15 || (MODE >= 17 && MODE <= 20)) {
       constexpr int aux = MODE != 3 ? 16 : 0;  // 16: sc1
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(cb, 0, kChunk * 3 / 2, 0x00020000);
       __builtin_amdgcn_raw_buffer_store_b128(v4u{w[0], w[1], w[2], w[3]}, rs, 16 * lane, 0, aux);
@@ -176,7 +191,7 @@ int main(int argc, char** argv) {
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
   const int ngroups = static_cast<int>(HW / (4 * kChunk));
-  for (int mode = 0; mode <= 16; ++mode) {
+  for (int mode = 0; mode <= 22; ++mode) {
     float best = 1e30f, sum = 0.f;
     for (int r = 0; r < 23; ++r) {
       (void)hipEventRecord(a, 0);
@@ -198,6 +213,12 @@ int main(int argc, char** argv) {
         case 14: hipLaunchKernelGGL(mix_k<14>, g, blk, 0, 0, st, HW, vs, ngroups, rec, hot); break;
         case 15: hipLaunchKernelGGL(mix_k<15>, g, blk, 0, 0, st, HW, vs, ngroups, rec, hot); break;
         case 16: hipLaunchKernelGGL(mix_k<16>, g, blk, 0, 0, st, HW, vs, ngroups, rec, hot); break;
+        case 17: hipLaunchKernelGGL(mix_k<17>, g, blk, 0, 0, st, HW, vs, ngroups, rec, hot); break;
+        case 18: hipLaunchKernelGGL(mix_k<18>, g, blk, 0, 0, st, HW, vs, ngroups, rec, hot); break;
+        case 19: hipLaunchKernelGGL(mix_k<19>, g, blk, 0, 0, st, HW, vs, ngroups, rec, hot); break;
+        case 20: hipLaunchKernelGGL(mix_k<20>, g, blk, 0, 0, st, HW, vs, ngroups, rec, hot); break;
+        case 21: hipLaunchKernelGGL(mix_k<21>, g, blk, 0, 0, st, HW, vs, ngroups, rec, hot); break;
+        case 22: hipLaunchKernelGGL(mix_k<22>, g, blk, 0, 0, st, HW, vs, ngroups, rec, hot); break;
         default:
           hipLaunchKernelGGL(copy_k, dim3(4 * n_cu), blk, 0, 0, reinterpret_cast<const v4u*>(st), reinterpret_cast<v4u*>(dst),
                              copy_bytes / 16);
@@ -211,7 +232,7 @@ int main(int argc, char** argv) {
         if (ms < best) best = ms;
       }
     }
-    const bool extra = mode != 0 && mode != 2 && mode != 8;
+    const bool extra = mode != 0 && mode != 2 && mode != 8 && mode != 21 && mode != 22;
     const double bytes = mode == 8 ? 2.0 * copy_bytes : (kNpl * static_cast<double>(HW) + (extra ? 1.5 * HW : 0.0)) * V;
     const double avg = sum / 20.0;
     printf("{\"views\": %d, \"px_per_view\": %lld, \"mode\": %d, \"best_us\": %.2f, \"avg_us\": %.2f, \"GBps_avg\": %.0f}\n", V,
