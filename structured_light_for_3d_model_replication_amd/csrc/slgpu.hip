@@ -78,6 +78,12 @@ constexpr bool kNtMaps = SLGPU_NT_MAPS != 0;  // non-temporal col/row map stores
 #ifndef SLGPU_NT_SIDE
 #define SLGPU_NT_SIDE 0
 #endif
+#ifndef SLGPU_NT_TEX
+#define SLGPU_NT_TEX 0  // (A/B) nt texture loads in k_cloud
+#endif
+#ifndef SLGPU_NT_STATS
+#define SLGPU_NT_STATS 0  // (A/B) nt loads in the histogram pass (k_stats, pre-stats)
+#endif
 constexpr bool kNtSide = SLGPU_NT_SIDE != 0;  // nt loads of records / texture / white-black in k_count, k_cloud
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
@@ -590,8 +596,16 @@ __device__ __forceinline__ void stats_pass(const uint8_t* vb, int64_t HW, int64_
   int mx = -1024;
   const int64_t n16 = HW / 16;  // HW % 16 == 0 on this path
   for (int64_t i = blk * kThreads + tid; i < n16; i += nblk * kThreads) {
-    const uint4 wq = *reinterpret_cast<const uint4*>(vb + 16 * i);
-    const uint4 bq = *reinterpret_cast<const uint4*>(vb + HW + 16 * i);
+    uint4 wq, bq;
+    if (SLGPU_NT_STATS) {  // (A/B) non-temporal white / black loads
+      const v4u a = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(vb + 16 * i));
+      const v4u b = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(vb + HW + 16 * i));
+      wq = make_uint4(a.x, a.y, a.z, a.w);
+      bq = make_uint4(b.x, b.y, b.z, b.w);
+    } else {
+      wq = *reinterpret_cast<const uint4*>(vb + 16 * i);
+      bq = *reinterpret_cast<const uint4*>(vb + HW + 16 * i);
+    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int bk = static_cast<int>(byte_of(bq, k));
@@ -1825,7 +1839,13 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
   uint4* tq = in->tq;
   if (p.tex != nullptr) {
     const uint8_t* t = p.tex + view * p.tex_vs + 3 * pxl;
-    if (vec) {
+    if (vec && SLGPU_NT_TEX) {  // (A/B) non-temporal texture loads (read once)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(t + 16 * i));
+        tq[i] = make_uint4(q.x, q.y, q.z, q.w);
+      }
+    } else if (vec) {
       tq[0] = ld_side16(t);
       tq[1] = ld_side16(t + 16);
       tq[2] = ld_side16(t + 32);
