@@ -1685,6 +1685,13 @@ constexpr int kBgrMode = SLGPU_LDS_BGR;
 constexpr bool kLdsBgr = kBgrMode == 1;
 constexpr bool kTexLds = kBgrMode == 2;
 constexpr int kBgrWords = kLdsBgr ? kChunk : kTexLds ? 3 * kChunk / 4 + 4 : 4;  // u32 per wave
+#ifndef SLGPU_TEX_COAL
+#define SLGPU_TEX_COAL 0
+#endif
+// k_cloud's texture loads as 1-KB rows of the chunk (each instruction whole
+// lines) instead of each lane's own 48 bytes (kTexLds only: the LDS copy is in
+// pixel order either way)
+constexpr bool kTexCoal = SLGPU_TEX_COAL != 0 && kTexLds;
 #ifndef SLGPU_COL_DWORD
 #define SLGPU_COL_DWORD 0
 #endif
@@ -1839,7 +1846,26 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
   uint4* tq = in->tq;
   if (p.tex != nullptr) {
     const uint8_t* t = p.tex + view * p.tex_vs + 3 * pxl;
-    if (vec && SLGPU_NT_TEX) {  // (A/B) non-temporal texture loads (read once)
+    if (vec && kTexCoal) {
+      // the chunk's 3 KB of texture as three 1-KB rows (lane: 16 B at 16 lane
+      // + 1024 i), so that each load instruction covers whole lines; k_cloud
+      // stores them to LDS at the same offsets (pixel order, kTexLds).  Rows
+      // past the view's texture (its last, partial chunk) re-read its last 16
+      // bytes: those pixels make no points.
+      const int64_t tv = 3 * HW;
+      const uint8_t* tb = p.tex + view * p.tex_vs;
+      const int64_t c0 = 3 * static_cast<int64_t>(civ) * kChunk + 16 * lane;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const uint8_t* a = tb + min<int64_t>(c0 + 1024 * i, tv - 16);
+        if (SLGPU_NT_TEX) {
+          const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(a));
+          tq[i] = make_uint4(q.x, q.y, q.z, q.w);
+        } else {
+          tq[i] = ld_side16(a);
+        }
+      }
+    } else if (vec && SLGPU_NT_TEX) {  // (A/B) non-temporal texture loads (read once)
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(t + 16 * i));
@@ -1910,7 +1936,11 @@ __device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long lo
   // ---- 2. compacted entries in LDS (and the chunk's colours, kTexLds) ----
   if (kTexLds) {
     uint4* t4 = reinterpret_cast<uint4*>(s_bgr);
-    if (has_tex) {
+    if (has_tex && kTexCoal && VEC > 0) {  // (cloud_load's 1-KB rows)
+      t4[lane] = tq[0];
+      t4[64 + lane] = tq[1];
+      t4[128 + lane] = tq[2];
+    } else if (has_tex) {
       t4[3 * lane] = tq[0];
       t4[3 * lane + 1] = tq[1];
       t4[3 * lane + 2] = tq[2];
@@ -2629,7 +2659,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_fused(Params p) {
     const int64_t pxl = (live && n_px > 0) ? px0 : 0;
     ChunkIn in;
     // the colour first: its latency overlaps the look-back
-    if (p.tex != nullptr) {
+    if (p.tex != nullptr && kTexCoal) {  // cloud_load's 1-KB rows (cloud_chunk's LDS order)
+      const uint8_t* tb = p.tex + view * p.tex_vs;
+      const int64_t c0 = 3 * static_cast<int64_t>(civ) * kChunk + 16 * lane;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) in.tq[i] = ld_side16(tb + min<int64_t>(c0 + 1024 * i, 3 * p.HW - 16));
+    } else if (p.tex != nullptr) {
       const uint8_t* t = p.tex + view * p.tex_vs + 3 * pxl;
       in.tq[0] = ld_side16(t);
       in.tq[1] = ld_side16(t + 16);
