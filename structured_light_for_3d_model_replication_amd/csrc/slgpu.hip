@@ -112,6 +112,14 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 // (measurement builds) k_decode's col / row / mask map stores as buffer stores
 // with this cache policy (16: sc1, write-through); 0: plain global stores
 constexpr int kMapAux = SLGPU_MAP_AUX;
+#ifndef SLGPU_MAP_STAGE
+#define SLGPU_MAP_STAGE 2
+#endif
+// k_decode's col / row map stores 1 KB contiguous per wave instruction through
+// a 1-KB LDS stage per wave (2: both maps, 1: the col map only), instead of
+// each lane's 64 B at a 64-B stride (0).  Config 2 120.3-120.6 -> 116.5-117.4
+// us per step, config 1 15.1 -> 14.4 (profiles/r04_ab/map_stage_lines.jsonl)
+constexpr bool kMapStage = SLGPU_MAP_STAGE != 0;
 // 16-byte store of 4 map words at p (16-byte aligned)
 __device__ __forceinline__ void st_map(int32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   const v4i v = {static_cast<int>(a), static_cast<int>(b), static_cast<int>(c), static_cast<int>(d)};
@@ -772,6 +780,8 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
   __shared__ unsigned s_bsum[kBsSlots];  // per iteration: points (low 16 bits) + waves arrived << 16
   __shared__ uint32_t s_thr[2];          // M_DECIDE adaptive: the view's tw2, tc2
   __shared__ unsigned s_mcount;          // M_DECIDE with p.masked: the workgroup's masked pixels
+  // kMapStage: a 1-KB stage per wave for contiguous map stores (maps kernels only)
+  __shared__ uint4 s_mapst[(kMapStage && (MODE < 0 || (MODE & M_MAPS))) ? 64 * kWaves : 1];
   unsigned* s_hist = s_lds;
   float4* s_pl = reinterpret_cast<float4*>(s_lds);
   const float* s_pl3 = reinterpret_cast<const float*>(s_lds);
@@ -1106,6 +1116,51 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
 #pragma unroll
             for (int e = 0; e < 4; ++e) r4[e] = kSwarGray ? row_code(i, e) : row[4 * i + e];
             __builtin_amdgcn_raw_buffer_store_b128(v4u{r4[0], r4[1], r4[2], r4[3]}, rr, bo + 16 * i, 0, kMapAux);
+          }
+        } else if (kMapStage && live) {
+          // 1-KB contiguous map stores through a 1-KB LDS stage per wave:
+          // for each quarter j of the chunk (pixels 256 j .. 256 j + 255, the
+          // 16 lanes of DPP row j), those lanes put their 64 B in the stage,
+          // then lane l stores bytes 16 l .. 16 l + 15 of it (pixels
+          // 256 j + 4 l ..); a lane stores only where its source lane's 16
+          // pixels are in the view (whole 16-pixel groups: W % 16 == 0)
+          uint4* const stg = s_mapst + 64 * wid;
+          const int64_t cbase = view * HW + static_cast<int64_t>(civ) * kChunk;  // the chunk's first pixel
+#pragma unroll
+          for (int m = 0; m < 2; ++m) {
+            if (m == 1 && SLGPU_MAP_STAGE == 1) {  // (1: the col map only; the rows as below)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                uint32_t r4[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) r4[e] = kSwarGray ? row_code(i, e) : row[4 * i + e];
+                if (n_px == kPx) st_map(p.row_out + o + 4 * i, r4[0], r4[1], r4[2], r4[3]);
+              }
+              continue;
+            }
+            // the chunk's 4 KB of this map as a buffer (SGPRs): stores past the
+            // view's end (its last, partial chunk) fall outside it and are dropped
+            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+                (m == 0 ? p.col_out : p.row_out) + cbase, 0,
+                static_cast<int>(4 * min<int64_t>(kChunk, HW - static_cast<int64_t>(civ) * kChunk)), 0x00020000);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if ((lane >> 4) == j && n_px == kPx) {
+                const int u = lane & 15;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                  uint32_t v4[4];
+#pragma unroll
+                  for (int e = 0; e < 4; ++e)
+                    v4[e] = m == 0 ? col[4 * q + e] : (kSwarGray ? row_code(q, e) : row[4 * q + e]);
+                  stg[4 * u + q] = make_uint4(v4[0], v4[1], v4[2], v4[3]);
+                }
+              }
+              __builtin_amdgcn_wave_barrier();
+              const uint4 v = stg[lane];
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rd, 1024 * j + 16 * lane, 0, 0);
+            }
           }
         } else if (n_px == kPx) {
 #pragma unroll
