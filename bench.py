@@ -114,11 +114,6 @@ def parse(argv=None):
     ap.add_argument("--cpu-procs", type=int, default=None,
                     help="processes of the multi-process CPU leg (default: the core share, multi-view "
                          "configs only; 0: off)")
-    ap.add_argument("--stack-ready", dest="stack_ready", action="store_true", default=False,
-                    help="declare the resident stacks ready on every call (sl_stack_ready: the histogram pass "
-                         "starts on a side stream beside the previous call's k_cloud; measured slower at c2, "
-                         "DESIGN.md 5.2)")
-    ap.add_argument("--no-stack-ready", dest="stack_ready", action="store_false")
     ap.add_argument("--next-stats", dest="next_stats", action="store_true", default=True,
                     help="every call names the next call's (resident) stack (sl_stack_next): its triangulation "
                          "kernel also computes the next call's adaptive-mask histograms (default)")
@@ -138,6 +133,14 @@ def parse(argv=None):
                     help="N > 1: also time BASELINE config 3 strong-scaled (36 views sharded over the N ranks) "
                          "and report it in multi_gpu.strong_c3 (default)")
     ap.add_argument("--no-strong-leg", dest="strong_leg", action="store_false")
+    ap.add_argument("--ring", type=int, default=1,
+                    help="one view in flight (c1 / c2): the headline window cycles through this many distinct "
+                         "resident views (stack, texture and outputs each), chained; 1 = the same view every step")
+    ap.add_argument("--ring-control", dest="ring_control", type=int, default=3,
+                    help="one view in flight: a second window with this many distinct views when the headline "
+                         "uses one (or one view when the headline cycles several), reported in "
+                         "timing.distinct_views -- does the 256 MB Infinity Cache help the one-view window? "
+                         "(0: off)")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
                          "scripts/traffic_from_pmc.py); default profiles/r04_traffic/traffic_<config>.json")
@@ -666,11 +669,6 @@ def main():
     # --xyz fast; SL_XYZ_F32_FAST applies without a pose (include/slgpu.h)
     head_fast = a.xyz == "fast" and poses is None
 
-    # the stacks are resident in HBM (written once, before the warm-up); with
-    # --stack-ready each call declares them ready (sl_stack_ready), so its
-    # histogram pass may start beside the previous call's k_cloud
-    ready = True if a.stack_ready else None
-
     # --next-stats (default): the next step reads the same resident stack, and
     # each call names it (sl_stack_next), so a call's k_cloud also runs the next
     # call's histogram pass and every call but the first starts with k_decode
@@ -678,8 +676,7 @@ def main():
 
     def step(o, maps=maps, fast=head_fast):
         eng.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
-                               xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o, stack_ready=ready,
-                               next_stack=nxt)
+                               xyz_dtype=torch.float32, poses=poses, fast_f32=fast, out=o, next_stack=nxt)
         return None
 
     # --streams S: core.ReconstructorPool, S contexts (own scratch, own
@@ -700,15 +697,38 @@ def main():
         torch.cuda.set_stream(torch.cuda.Stream(dev))
     cur = torch.cuda.current_stream(dev)
 
+    # one view in flight: the steps cycle through ring["R"] resident views
+    # (slot 0 = the view above; --ring / --ring-control add distinct ones, each
+    # with its own stack, texture and outputs), every call naming the next
+    # slot's stack (sl_stack_next)
+    ring = {"R": 1, "i": 0}
+    slots = [dict(stack=stack, tex=tex, out=out)]
+    ring_R = max(1, a.ring) if pool is None and V == 1 else 1
+    ctl_R = 0
+    if pool is None and V == 1 and a.ring_control > 0:
+        ctl_R = a.ring_control if ring_R == 1 else 1
+    for k in range(1, max(ring_R, ctl_R)):
+        s_, t_ = synth.render_stack(rig, seed=1000 * cfg_idx + 500 + k, include_rows=rows,
+                                    view_deg=cfg["deg"] * (views[0] + 7 * k), device=dev)
+        slots.append(dict(stack=s_[None].contiguous(), tex=t_[None].contiguous(), out={}))
+        del s_, t_
+    ring["R"] = ring_R
+
     def one():
         """One step; -> the stream it ran on."""
         if pool is None:
-            step(out)
+            R = ring["R"]
+            i = ring["i"] % R
+            ring["i"] += 1
+            sl, nx = slots[i], slots[(i + 1) % R]
+            eng.decode_triangulate(sl["stack"], n_cols, n_rows, texture=sl["tex"], maps=maps, cloud=True,
+                                   xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast, out=sl["out"],
+                                   next_stack=nx["stack"] if a.next_stats else None)
             return cur
         res = pool.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
                                       xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
                                       wait_inputs=False,  # resident inputs; outputs never read meanwhile
-                                      stack_ready=ready, next_stack=nxt)
+                                      next_stack=nxt)
         return res["stream"]
 
     def run_steps(k):
@@ -718,9 +738,17 @@ def main():
     def sync_all():
         torch.cuda.synchronize(dev)
 
-    run_steps(max(a.warmup, S))
+    for R in sorted({len(slots), ring_R}):  # every slot's outputs allocated before any window
+        ring["R"] = R
+        run_steps(max(a.warmup, S, R))
+    ring["R"] = ring_R
     sync_all()
-    n_pts = int(out["view_offsets"][-1].item())
+    # points per step: the mean over the views the headline cycles through
+    n_pts = sum(int(sl["out"]["view_offsets"][-1].item()) for sl in slots[:ring_R]) / ring_R
+
+    def end_on_slot0(k):
+        """The next k steps end on slot 0 (whose outputs the verified sample copies)."""
+        ring["i"] = (1 - k) % ring["R"]
 
     def timed(k, evs=None):
         """K steps between barrier + synchronize pairs; with ``evs`` (k+1
@@ -802,6 +830,7 @@ def main():
         pre = preroll(a.preroll_ms)
         window = {"mode": "eager: K calls enqueued inside the window"}
         graph_keep = None
+        end_on_slot0(a.steps)
         if a.graph and pool is None:
             try:
                 el_rank, graph_keep, cap_ms = timed_graph(a.steps)
@@ -819,6 +848,35 @@ def main():
         if snap is not None:  # the headline window's last step (the next window's sync waits for the copies)
             snap_copy(snap, out, cur)
         el_ev, step_us = timed(a.steps, evs)
+        # the control window: the same K steps over ctl_R distinct resident
+        # views (or one, when the headline cycles several), after its own
+        # pre-roll, captured and launched as the headline -- do the 256 MB
+        # Infinity Cache's hits on one view's texture, records and outputs
+        # from step to step make the one-view headline faster?
+        distinct = None
+        if ctl_R:
+            ring["R"] = ctl_R
+            pre2 = preroll(a.preroll_ms)
+            end_on_slot0(a.steps)
+            mode2 = "eager"
+            if a.graph:
+                try:
+                    el_ctl, graph_keep2, _ = timed_graph(a.steps)
+                    mode2 = "hipGraph, as the headline"
+                except Exception as e:  # noqa: BLE001
+                    torch.cuda.synchronize(dev)
+                    eng.drop_next()
+                    el_ctl, _ = timed(a.steps)
+                    mode2 = "eager (graph capture failed: %s)" % (str(e)[:120],)
+            else:
+                el_ctl, _ = timed(a.steps)
+            snap2 = snap_alloc(out, V, maps) if snap is not None else None
+            if snap2 is not None:
+                snap_copy(snap2, out, cur)
+            resident = sum(sl["stack"].numel() + sl["tex"].numel() for sl in slots[:ctl_R])
+            distinct = {"views": ctl_R, "ms_per_step": 1e3 * el_ctl / a.steps, "window": mode2,
+                        "preroll": pre2, "resident_input_bytes": int(resident), "snap": snap2}
+            ring["R"] = ring_R
     finally:
         gc.enable()
     t = torch.tensor([el_rank], dtype=torch.float64, device=dev)
@@ -919,6 +977,10 @@ def main():
     verified, verification = None, None
     if snap is not None:
         verified, verification = verify(snap, stack, tex, poses, calib, n_cols, n_rows, head_fast)
+        if distinct is not None and distinct.get("snap") is not None:
+            ok2, ver2 = verify(distinct["snap"], stack, tex, poses, calib, n_cols, n_rows, head_fast)
+            verification["distinct_views_window"] = ver2
+            verified = verified and ok2
         if distributed:
             f = torch.tensor([1 if verified else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(f, op=dist.ReduceOp.MIN)
@@ -975,7 +1037,7 @@ def main():
                                    + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
                        "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
                        "parallelism": f"views sharded over {world} GPU(s)", "streams_per_gpu": S,
-                       "stack_ready": bool(a.stack_ready), "next_stats": bool(a.next_stats)},
+                       "next_stats": bool(a.next_stats)},
             "timing": {"preroll": pre,
                        "step_us": spread(step_us),
                        "step_us_note": "HIP events at every step boundary, on the step's stream; intervals "
@@ -987,7 +1049,18 @@ def main():
                        "host_enqueue_ms": enq_ms,
                        "host_enqueue_note": "host time to enqueue the headline window's K steps (of its wall "
                                             "time): close to the wall time = the host, not the GPU, set the pace",
-                       "gc": "collected before the pre-roll, disabled through the windows"},
+                       "gc": "collected before the pre-roll, disabled through the windows",
+                       "ring_views": ring_R,
+                       "distinct_views": None if distinct is None else {
+                           "views": distinct["views"], "ms_per_step": distinct["ms_per_step"],
+                           "ratio_to_headline": distinct["ms_per_step"] / (1e3 * el / a.steps),
+                           "window": distinct["window"], "preroll": distinct["preroll"],
+                           "resident_input_bytes": distinct["resident_input_bytes"],
+                           "note": "the same K chained steps cycling through this many distinct resident views "
+                                   "(stack, texture and outputs each), after their own pre-roll: > 1 view puts "
+                                   "more than the 256 MB Infinity Cache between a view's steps, so no texture, "
+                                   "record or output line of a view survives to its next step; verified like "
+                                   "the headline (verification.distinct_views_window)"}},
             "roofline": {"bound": "hbm", "scope": "whole path per step: every kernel of the step",
                          "achieved": path_gbps, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": path_gbps / HBM_PEAK_GBS, "traffic": traffic,

@@ -40,8 +40,7 @@ extern "C" {
                              sl_system.py:553-554                                      */
 #define SL_EHIP (-3)      /* HIP runtime failure -> RuntimeError                        */
 #define SL_ENOCALIB (-4)  /* sl_set_calib not called / shape mismatch -> ValueError       */
-#define SL_ETIMEOUT (-5)  /* reserved (the one device-side wait, k_fused's bounded look-back,
-                             reports a give-up as a view_offsets total of -1)           */
+#define SL_ETIMEOUT (-5)  /* reserved                                                     */
 #define SL_ECAPACITY (-6) /* output capacity smaller than the pixel count -> ValueError   */
 #define SL_EIO (-7)       /* file could not be written -> OSError                        */
 
@@ -71,16 +70,18 @@ void sl_ctx_destroy(sl_ctx* ctx);
 const char* sl_ctx_last_error(const sl_ctx* ctx);
 
 /* Pre-size the context's scratch for up to `max_views` views of `max_px`
- * pixels each so that later calls allocate nothing (required before stream
- * capture into a hipGraph).  Calls grow scratch on demand otherwise.
- * Graphs: a context rotates part of its scratch from launch group to launch
- * group without host work (block-sum buffers over 2, the pre-stats
- * histograms of sl_stack_next over 3, the adaptive-mask histograms of
- * k_stats over 2), so a captured sequence of calls replays correctly right
- * after its capture; it replays again and again only when it holds a
- * multiple of 6 launch groups (each rotation back at its start).  An
- * out-of-phase replay writes no point past out_capacity (the cloud's total in
- * view_offsets then exceeds it) but its results are invalid. */
+ * pixels each (and the histograms of a whole launch group) so that later calls
+ * allocate nothing (required before stream capture into a hipGraph).  Calls
+ * grow scratch on demand otherwise.
+ * Graphs: any sequence of calls captured on one stream replays any number of
+ * times, in any order with other work on the context.  The scratch a launch
+ * accumulates into (block sums, the adaptive mask's histograms) is zero at
+ * every launch-group boundary -- the kernel that consumes it zeroes it, on the
+ * device, once its last reader is done -- and the one thing that crosses a
+ * call boundary, a histogram pass queued by sl_stack_next, is taken only by a
+ * call in the same capture (a graph's first call therefore runs its own
+ * histogram pass; a pass the graph's last call queues is cleared by the
+ * next call that does not take it). */
 int sl_ctx_reserve(sl_ctx* ctx, int64_t max_views, int64_t max_px);
 
 /* Upload calibration for an H x W camera (the calib.mat fields loaded at
@@ -139,18 +140,12 @@ int sl_decode_triangulate(sl_ctx* ctx, const uint8_t* stack, int64_t stack_view_
 int sl_mask_counts_to(sl_ctx* ctx, int64_t* device_counts);
 
 /* Stack readiness for the NEXT sl_decode_triangulate on this context (that
- * call only; consumed even when the call fails): the caller promises that the
- * stack and texture are in place once `event` (a hipEvent_t recorded by the
- * caller) has completed, or already now when `event` is NULL (stacks resident
- * in HBM, or written by work the caller has synchronised).  The call's
- * adaptive-mask histogram pass (sl_system.py:526-528) then runs on the
- * context's side stream as soon as that holds and the previous call's decode
- * has read its own histograms -- beside the previous call's triangulation --
- * instead of behind everything queued on the call's stream.  Results are
- * unchanged.  (The later launch groups of one large call need no such
- * promise: each takes its histograms from a pass the previous group's k_cloud
- * ran -- pre-stats within the call.)  Not applied while the call's stream is
- * being captured into a graph. */
+ * call only; consumed even when the call fails): the stack and texture are in
+ * place once `event` (a hipEvent_t recorded by the caller) has completed --
+ * the call's work waits for it on its stream -- or already now when `event`
+ * is NULL.  Results are unchanged.  (Round 3 ran the histogram pass of such a
+ * call on a side stream beside the previous call's triangulation: measured
+ * slower than sl_stack_next's pre-stats, DESIGN.md 5.2, and removed.) */
 int sl_stack_ready(sl_ctx* ctx, void* event);
 
 /* The call AFTER the coming one (a stream of views): arms the NEXT
@@ -160,9 +155,10 @@ int sl_stack_ready(sl_ctx* ctx, void* event);
  * first launch group of `stack` [n_views][...] (view stride stack_view_stride,
  * 16-byte aligned, the same frame size as the coming call).  The call after it
  * then starts with its decode -- when it is on this context, reads that same
- * stack pointer, stride, view count and frame size with the adaptive mask, and
- * nothing ran on the context in between; otherwise it computes its histograms
- * itself.  The caller promises that `stack` holds the next call's images, in
+ * stack pointer, stride, view count and frame size with the adaptive mask,
+ * nothing ran on the context in between, and both calls are enqueued in the
+ * same stream capture (or both outside one); otherwise it computes its
+ * histograms itself.  The caller promises that `stack` holds the next call's images, in
  * place by the time the coming call's work starts on its stream, and unchanged
  * until the next call.  Results are unchanged.  NULL disarms, and also drops a
  * pass an earlier call queued for the next one (that call then computes its
@@ -220,8 +216,7 @@ int sl_profile_enable(sl_ctx* ctx, int max_calls);
 int sl_profile_read(sl_ctx* ctx, double* decode_ms, double* count_ms, double* cloud_ms, int* calls);
 
 /* The last call's kernel path -- 0: k_decode + k_count + k_cloud; 1: [k_stats]
- * + k_decode + k_cloud, k_decode applying the mask and the point decision;
- * 2: [k_stats] + k_fused (decode and cloud in one launch, SLGPU_FUSED=1)
+ * + k_decode + k_cloud, k_decode applying the mask and the point decision
  * (frames with W % 16 == 0, W, H <= 4096 and Wp <= 2048; sl_profile_* and
  * sl_time_kernels then report k_stats in the k_count slot) -- its number of
  * launch groups, and the pixels of its last launch group (what
@@ -232,9 +227,11 @@ int sl_last_launch_info(sl_ctx* ctx, int* path, int64_t* launches, int64_t* last
  * of the previous sl_decode_triangulate / sl_triangulate_maps call `reps`
  * times each, back to back on its stream, and returns each kernel's average
  * duration from HIP events around the `reps` launches (the events' own cost
- * amortised).  k_count and k_cloud run first: the call's outputs are rewritten
- * with the same values; the adaptive-threshold histograms k_decode's re-runs
- * accumulate into are reset for later calls. */
+ * amortised).  The inputs the call consumed (histograms, block sums) are
+ * rebuilt once first, untimed; k_cloud and k_count run first: the call's
+ * outputs are rewritten with the same values.  Afterwards the context's
+ * scratch is clean again: a histogram pass queued by sl_stack_next is dropped
+ * (the next call computes its own). */
 int sl_time_kernels(sl_ctx* ctx, int reps, double* decode_ms, double* count_ms, double* cloud_ms);
 
 /* ASCII PLY of a cloud exactly as the reference writes it (sl_system.py:665-691,

@@ -56,8 +56,7 @@ class Cloud:
         n = int(self.view_offsets[-1].item())
         if not 0 <= n <= self.xyz.shape[0]:
             raise RuntimeError(f"cloud total {n} is outside the output capacity {self.xyz.shape[0]}: the "
-                               "context's scratch was out of phase with this call (e.g. a captured graph replayed "
-                               "with a launch count that is not a multiple of 6, include/slgpu.h)")
+                               "output buffer was written by another call, or the call failed")
         return n
 
 
@@ -186,11 +185,9 @@ class Reconstructor:
         view's number of pixels that pass the mask -- the N of
         reconstruct_point_cloud's "Processing N valid pixels..." line
         (sl_system.py:601-602) -- asynchronously, like the other outputs.
-        ``stack_ready`` (``True`` or a ``torch.cuda.Event``): the caller's
-        promise that the stack and texture are in place now (resident in HBM)
-        or once that event has completed, whatever is queued on ``stream``;
-        the adaptive mask's histogram pass then starts on the context's side
-        stream beside the previous call's triangulation (sl_stack_ready).
+        ``stack_ready`` (``True`` or a ``torch.cuda.Event``): the stack and
+        texture are in place now, or once that event has completed -- the
+        call's work on ``stream`` waits for it (sl_stack_ready).
         ``next_stack`` (uint8, same frame size, contiguous frames, on this
         device): the stack of the NEXT call on this reconstructor, already in
         place by the time this call's work starts on ``stream`` and unchanged

@@ -11,22 +11,28 @@
 // Work unit: a CHUNK of 1024 consecutive pixels of one view, owned by one wave.
 // A 256-thread workgroup is 4 chunks of one view; grid = (chunk groups, views).
 //
-// Three kernels on one HIP stream, no host synchronisation between them:
-//   k_decode : streams the uint8 stack once (16-byte loads, lane = 16 contiguous
-//              pixels), forms the Gray bits with a byte-SWAR compare, Gray ->
-//              binary in registers; writes the col/row maps and a 2-byte record
-//              (clipped column code) per pixel.  Adaptive mask: also the 256-bin
-//              histogram of the black plane + max(white - black), per workgroup
-//              in LDS, added to the view's histogram at the end.
-//   k_count  : per wave, the float32 np.percentile(black, 95) thresholds from
-//              the histogram; the mask of every pixel (mask map) and, for the
-//              cloud, the |n.r| > 1e-6 decision (f32 with an exact error bound,
-//              f64 where undecided) as a point bitmask + the chunk's point count
-//              (also added to its 64-chunk super-block sum).
-//   k_cloud  : the chunk's output offset from the super-block and chunk sums,
-//              its points compacted in LDS, the ray/plane intersection in f64
-//              (reference operation order, no contraction), and the stores at
-//              offset + rank -- the reference's np.where order.
+// Default path (aligned frames, decision tables in LDS), per launch group on
+// one HIP stream, no host synchronisation between the kernels:
+//   k_stats  : (adaptive mask) the black-plane histogram + max(white - black)
+//              of every view -- or the same pass run by the previous call's
+//              k_cloud (pre-stats, sl_stack_next);
+//   k_decode : streams the uint8 stack once, Gray bits by byte-SWAR compares,
+//              Gray -> binary in the byte lanes; col/row/mask maps, the mask
+//              and the |n.r| > 1e-6 decision, 12-bit records, block sums;
+//   k_cloud  : the chunk's output offset from the super-block and block sums,
+//              its points compacted in LDS, the ray/plane intersection in the
+//              reference's f64 order (or its proven-equal verified form), the
+//              stores at offset + rank -- the reference's np.where order.
+// Frames that do not fit it (unaligned, W or H > 4096, Wp > 2048) run
+// k_decode (codes + histogram) -> k_count (mask, decision) -> k_cloud.
+//
+// Scratch is clean at every launch-group boundary, whatever ran before: the
+// kernel that consumes an accumulated buffer (k_decode / k_count the
+// histograms, k_cloud the super-block sums) zeroes it once its last reader is
+// done (a per-buffer arrival counter), so a captured hipGraph replays in any
+// phase.  The one thing that crosses a boundary is a pre-stats pass queued for
+// the next call, which the host hands on only within one capture (or eager
+// call sequence).
 //
 // Everything in this file is compiled with -ffp-contract=off.
 #include <hip/hip_runtime.h>
@@ -62,70 +68,18 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kPx = 16;                 // pixels per lane in the streaming layout
 constexpr int kChunk = 64 * kPx;        // pixels per wave (one chunk)
 constexpr int kChunkNib = kChunk / 4;   // point-nibble bytes per chunk
-#ifndef SLGPU_RING
-#define SLGPU_RING 40
-#endif
-constexpr int kRing = SLGPU_RING;       // stack planes in flight per lane
-#ifndef SLGPU_LOAD_AUX
-#define SLGPU_LOAD_AUX 2
-#endif
-constexpr int kLoadAux = SLGPU_LOAD_AUX;  // cache policy of the stack loads (2 = nt)
-#ifndef SLGPU_NT_MAPS
-#define SLGPU_NT_MAPS 0
-#endif
-constexpr bool kNtMaps = SLGPU_NT_MAPS != 0;  // non-temporal col/row map stores
-
-#ifndef SLGPU_NT_SIDE
-#define SLGPU_NT_SIDE 0
-#endif
-#ifndef SLGPU_NT_TEX
-#define SLGPU_NT_TEX 0  // (A/B) nt texture loads in k_cloud
-#endif
-#ifndef SLGPU_NT_STATS
-#define SLGPU_NT_STATS 0  // (A/B) nt loads in the histogram pass (k_stats, pre-stats)
-#endif
-constexpr bool kNtSide = SLGPU_NT_SIDE != 0;  // nt loads of records / texture / white-black in k_count, k_cloud
+constexpr int kRing = 40;               // stack planes in flight per lane
+// Cache policies (measured): the stack streams with nt loads
+// (aux 2); the side loads (records, texture, the histogram pass's white and
+// black) keep the default policy, whose lines the next kernel finds in the
+// Infinity Cache; cloud-only records leave write-through (sc1, aux 16).
+constexpr int kLoadAux = 2;
+constexpr int kRecAux = 16;
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint4 ld_side16(const void* p) {
-  if (kNtSide) {
-    const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-  }
-  return *reinterpret_cast<const uint4*>(p);
-}
-__device__ __forceinline__ uint2 ld_side8(const void* p) {
-  if (kNtSide) {
-    const v2u v = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
-    return make_uint2(v.x, v.y);
-  }
-  return *reinterpret_cast<const uint2*>(p);
-}
-__device__ __forceinline__ uint32_t ld_side4(const void* p) {
-  if (kNtSide) return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
-  return *reinterpret_cast<const uint32_t*>(p);
-}
-typedef int v4i __attribute__((ext_vector_type(4)));
-#ifndef SLGPU_MAP_AUX
-#define SLGPU_MAP_AUX 0
-#endif
-// (measurement builds) k_decode's col / row / mask map stores as buffer stores
-// with this cache policy (16: sc1, write-through); 0: plain global stores
-constexpr int kMapAux = SLGPU_MAP_AUX;
-#ifndef SLGPU_MAP_STAGE
-#define SLGPU_MAP_STAGE 2
-#endif
-// k_decode's col / row map stores 1 KB contiguous per wave instruction through
-// a 1-KB LDS stage per wave (2: both maps, 1: the col map only), instead of
-// each lane's 64 B at a 64-B stride (0).  Config 2 120.3-120.6 -> 116.5-117.4
-// us per step, config 1 15.1 -> 14.4 (profiles/r04_ab/map_stage_lines.jsonl)
-constexpr bool kMapStage = SLGPU_MAP_STAGE != 0;
-// 16-byte store of 4 map words at p (16-byte aligned)
-__device__ __forceinline__ void st_map(int32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  const v4i v = {static_cast<int>(a), static_cast<int>(b), static_cast<int>(c), static_cast<int>(d)};
-  if (kNtMaps) __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(p));
-  else *reinterpret_cast<v4i*>(p) = v;
-}
+__device__ __forceinline__ uint4 ld_side16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ uint2 ld_side8(const void* p) { return *reinterpret_cast<const uint2*>(p); }
+__device__ __forceinline__ uint32_t ld_side4(const void* p) { return *reinterpret_cast<const uint32_t*>(p); }
 
 // mode bits
 constexpr int M_MAPS = 1;      // k_decode: col/row maps; k_count: mask map
@@ -141,54 +95,20 @@ constexpr int M_TEX = 2048;    // k_cloud: a BGR texture (else the white plane r
 constexpr int M_VERIFY = 4096; // k_cloud, SL_XYZ_F32: a shorter f64 evaluation whose f32 rounding is proven equal
                                // to the reference's (else the operators' sequences); Oc = 0, pinhole rays
                                // (with or without a pose)
-constexpr int M_FUSED = 1024;  // k_fused: k_decode's chunk group, then its cloud (look-back offsets) in one launch
 constexpr int M_DECIDE = 256;  // k_decode: also the mask and the |n.r| decision (k_count's work; k_stats
-                               // histograms): mask map, point nibbles, chunk counts, block sums
+                               // histograms): mask map, 12-bit records, chunk counts, block sums
 constexpr float kFastKappa = 16.0f;  // condition-number limit of the f32 route
 
-constexpr int kSlot = 272;                 // histogram of one view: 256 bins + max + pad (u32)
-#ifndef SLGPU_HIST_REP
-#define SLGPU_HIST_REP 8
-#endif
-constexpr int kHistRep = SLGPU_HIST_REP;   // LDS histogram replicas (lane % kHistRep; 8 measured best of 1/4/8/16/32/64)
+constexpr int kSlot = 272;      // histogram of one view: 256 bins + max + arrival counters + pad (u32)
+constexpr int kSlotArrive = 257;  // ... its readers' two-level arrival counter (9 words, arrive_last<8>)
+constexpr int kHistRep = 8;     // LDS histogram replicas (lane % kHistRep; 8 measured best of 1/4/8/16/32/64)
 constexpr int kHistStride = kHistRep + 1;  // bin stride: replica r of bin b sits in bank (b + r) % 32
-// Measurement-only ablations, compiled in only by -DSLGPU_ABLATE=<bits> (a
-// separate build for scripts/, never the shipped library): 1 = k_cloud without
-// point math, 2 = k_cloud without xyz/colour stores, 4 = k_cloud without
-// operand gathers, 8 = k_cloud stops after its loads + rank scan, 16 = ... after
-// the LDS compaction, 32 = k_count with the fixed thresholds, 64 = k_count
-// without the |n.r| test, 128 = k_count without plane gathers, 1024 = exact k_cloud gathers
-// its planes from a 32-entry table (cache footprint), 4096 = exact k_cloud without any point
-// arithmetic, 8192 = k_cloud without its block prefix (each chunk writes at 1024 x its index),
-// 16384 / 32768 = the exact k_cloud without its colour / xyz stores.
-#ifndef SLGPU_ABLATE
-#define SLGPU_ABLATE 0
-#endif
-constexpr int kAblate = SLGPU_ABLATE;
-#ifndef SLGPU_XY_CALC
-#define SLGPU_XY_CALC 1
-#endif
-constexpr bool kXyCalc = SLGPU_XY_CALC != 0;  // exact k_cloud: rays' x / y by xy_of where sl_set_calib verified it
 constexpr int kMaxWp = 32768;              // projector columns (record codes are 15 bits)
-#ifndef SLGPU_MAX_CHUNKS
-#define SLGPU_MAX_CHUNKS (1 << 16)
-#endif
-constexpr int64_t kMaxChunks = SLGPU_MAX_CHUNKS;  // chunks per launch group: bounds k_cloud's prefix reads
-#ifndef SLGPU_REC_BLK
-#define SLGPU_REC_BLK 1
-#endif
-// 12-bit records in chunk slots (1536 B: a lane's 16 codes as 16 B at 16 lane
-// + 8 B at 1024 + 8 lane), the launch group's views interleaved by chunk group
-// (rec_slot), stored write-through (kRecAux = sc1).  0: pixel order, 24 B per
-// lane as two 12-B stores (A/B; scripts/micro/write_mix.hip prices both shapes)
-constexpr bool kRecBlk = SLGPU_REC_BLK != 0;
-#ifndef SLGPU_REC_BLK_MAPS
-#define SLGPU_REC_BLK_MAPS 0  // (A/B) chunk slots in the maps kernels too
-#endif
-#ifndef SLGPU_REC_AUX
-#define SLGPU_REC_AUX 16
-#endif
-constexpr int kRecAux = SLGPU_REC_AUX;
+constexpr int64_t kMaxChunks = 1 << 16;    // chunks per launch group: bounds k_cloud's prefix reads
+// Cloud-only calls keep the 12-bit records in chunk slots (1536 B: a lane's 16
+// codes as 16 B at 16 lane + 8 B at 1024 + 8 lane), the launch group's views
+// interleaved by chunk group (rec_slot), stored write-through; calls with maps
+// keep pixel order, 24 B per lane as two 12-B stores (their registers fit).
 constexpr int kRecSlot = 1536;
 
 struct ViewStats {
@@ -223,7 +143,6 @@ struct Params {
   int Wp;
   const double4* planes;   // (n0, n1, n2, num = n.Oc + d) per projector column
   const float4* planes32;  // f32 (n0, n1, n2, -) for the point/no-point pre-decision
-  const float* planes12;   // the same (n0, n1, n2) packed, 12 B per column (+ 1 KB of slack)
   const double* xn;        // (u - cx) / fx
   const double* yn;        // (v - cy) / fy
   const float* xn32;
@@ -238,11 +157,9 @@ struct Params {
   double o0, o1, o2;       // Oc
   const double* poses;
   uint16_t* codes;   // [view][HW] records: min(col, Wp-1)
-  const int32_t* rec_col;  // maps + cloud on the decide path: k_cloud takes min(col, Wp-1) from this col
-  int rec12;               // decide path (Wp < 4096): records packed 12 bits per pixel, 24 B per 16
+  int rec12;               // decide path (Wp <= 2048): records packed 12 bits per pixel, 24 B per 16
                            // pixels, code 0xfff = no point (1.5 B/px written, no point nibbles)
-                           // map and k_decode writes no records (2 B/px less k_decode write traffic)
-  int rec_blk;             // rec12 records in kRecBlk's chunk slots (k_decode without maps; else pixel order)
+  int rec_blk;             // rec12 records in chunk slots (k_decode without maps; else pixel order)
   uint8_t* ptnib;    // [chunk][4 steps][64 lanes] point nibbles: bit e of byte (s, l) = pixel 256 s + 4 l + e
   int32_t* col_out;
   int32_t* row_out;
@@ -254,36 +171,35 @@ struct Params {
   ViewStats* stats;
   unsigned long long* masked;  // or null: += masked pixels of each view (sl_mask_counts_to; the
                                // "Processing N valid pixels..." of sl_system.py:601-602)
-  unsigned* hist;       // [view][kSlot] accumulated by this launch's k_decode
-  unsigned* hist_zero;  // [view][kSlot] zeroed by this launch's k_decode (the next launch's hist)
+  // the adaptive mask's histograms: [view][kHistView] (decide path, k_stats /
+  // pre-stats replicas) or [view][kSlot] (3-kernel path, k_decode's); clean
+  // before the producing launch, zeroed by the consuming kernel's last reader
+  // of each view (arrival counter at word kSlotArrive of the view's first slot)
+  unsigned* hist;
   const int64_t* base_in;  // points of the earlier launch groups of this call, or null
   int* chunk_counts;       // k_count -> k_cloud: points per chunk
   int* block_sums;         // k_count -> k_cloud: points per workgroup (4 chunks)
   int bs_atomic;           // k_decode M_DECIDE: block sums by the last wave to arrive (no barrier)
   int decode_dyn;          // k_decode M_DECIDE | M_CODES: chunk groups after the first round pulled from a
-                           // per-view counter (super_sums' last entries), not strided (SLGPU_DECODE_DYN=1, A/B)
+                           // per-view counter (super_sums' last entries), not strided (cloud-only calls)
   // two-level block prefix: every block (workgroup of 4 chunks) also adds its
-  // sum to super_sums[block >> sb_shift]; k_cloud's offset = the super-block
-  // sums before its super-block + the block sums before it inside it
-  unsigned* super_sums;    // zeroed before the launch (by the previous launch's k_decode)
-  unsigned* super_zero;    // the next launch's super-block sums: zeroed by this launch's k_decode
-  int super_cap;           // entries of each super buffer
+  // sum to super[block >> sb_shift]; k_cloud's offset = the super-block sums
+  // before its super-block + the block sums before it inside it.  Two buffers
+  // of kSuperCap words (super-block sums + the dynamic grid's counters, their
+  // last n_views entries) at super_base, selected on the device (super_sel).
+  unsigned* super_base;
+  unsigned* super_par;     // [0]: the buffer the next producer accumulates into, [1]: the one k_cloud reads
   int sb_shift;
-  unsigned long long* lb;  // k_fused: look-back granules, one per workgroup of the launch (zeroed before it)
-  int64_t lb_n;            // ... their number (k_stats zeroes them)
+  int rerun;               // sl_time_kernels' re-runs: consumers leave their inputs as they are
   int cloud_gx;            // k_cloud: workgroups per view that triangulate (the grid's x beyond: pre-stats)
   // k_cloud's pre-stats workgroups (sl_stack_next): the NEXT call's histogram
   // pass (k_stats' work) for the views of its first launch group, beside this
   // call's triangulation; null pre_stack: none
   const uint8_t* pre_stack;
   int64_t pre_vs;
-  unsigned* pre_hist;      // [pre_views][kHistView] accumulated (zero before the launch)
-  unsigned* pre_zero;      // the following pre-stats buffer: its first pre_zero_words words zeroed
-  int64_t pre_zero_words;
+  unsigned* pre_hist;      // [pre_views][kHistView] accumulated (clean before the launch)
   int pre_views;           // views of the next call's first group
   int pre_bpv;             // workgroups per view (k_stats' grid x)
-  int pre_mix;             // pre-stats workgroups spread among the triangulating ones (else after them)
-  int decode_gx;           // k_decode: decoding workgroups per view (0: gridDim.x; beyond: pre-stats)
 };
 
 // ---------------------------------------------------------------- helpers ----
@@ -397,10 +313,6 @@ __device__ __forceinline__ long long uniform64(long long v) {
 // bits.  The reciprocal step depends on b only, so divisions by one b share
 // it.  div_safe(v): v is such an operand (and not +-0, whose sign the
 // residual step would lose).
-#ifndef SLGPU_DIV_SHARE
-#define SLGPU_DIV_SHARE 1
-#endif
-constexpr bool kDivShare = SLGPU_DIV_SHARE != 0;
 __device__ __forceinline__ double recip_nr(double b) {
   double r = __builtin_amdgcn_rcp(b);
   double e = __builtin_fma(-b, r, 1.0);
@@ -604,16 +516,8 @@ __device__ __forceinline__ void stats_pass(const uint8_t* vb, int64_t HW, int64_
   int mx = -1024;
   const int64_t n16 = HW / 16;  // HW % 16 == 0 on this path
   for (int64_t i = blk * kThreads + tid; i < n16; i += nblk * kThreads) {
-    uint4 wq, bq;
-    if (SLGPU_NT_STATS) {  // (A/B) non-temporal white / black loads
-      const v4u a = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(vb + 16 * i));
-      const v4u b = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(vb + HW + 16 * i));
-      wq = make_uint4(a.x, a.y, a.z, a.w);
-      bq = make_uint4(b.x, b.y, b.z, b.w);
-    } else {
-      wq = *reinterpret_cast<const uint4*>(vb + 16 * i);
-      bq = *reinterpret_cast<const uint4*>(vb + HW + 16 * i);
-    }
+    const uint4 wq = ld_side16(vb + 16 * i);
+    const uint4 bq = ld_side16(vb + HW + 16 * i);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int bk = static_cast<int>(byte_of(bq, k));
@@ -640,30 +544,22 @@ __device__ __forceinline__ void stats_pass(const uint8_t* vb, int64_t HW, int64_
 }
 
 // grid (blocks per view, views of the group); 16 pixels per thread per step.
+// p.hist is clean (the last consumer zeroed it, or the host did).
 __global__ __launch_bounds__(kThreads) void k_stats(Params p) {
   __shared__ unsigned s_hist[256 * kHistStride];
   __shared__ int s_max[kWaves];
-  const int tid = threadIdx.x;
   const int view = blockIdx.y;
-  if (blockIdx.x == 0)  // the next launch group's histograms of this slot (its scratch here)
-    for (int i = tid; i < kHistView; i += kThreads) p.hist_zero[static_cast<int64_t>(view) * kHistView + i] = 0u;
-  if (p.lb && blockIdx.x == 0 && view == 0)  // k_fused's look-back granules (it follows this launch)
-    for (int64_t i = tid; i < p.lb_n; i += kThreads) p.lb[i] = 0ull;
   stats_pass(p.stack + view * p.stack_vs, p.HW, blockIdx.x, gridDim.x, p.hist + static_cast<int64_t>(view) * kHistView,
              s_hist, s_max);
 }
 
 // One pre-stats workgroup (sl_stack_next), number sx of the nsx per grid row
-// that a k_cloud or k_decode launch appends: zeroes its share of the buffer
-// the following pass accumulates into, then runs its share of the next call's
-// histogram pass (k_stats' work) into p.pre_hist.
+// that a k_cloud launch appends: its share of the next call's histogram pass
+// (k_stats' work) into p.pre_hist.
 __device__ __forceinline__ void pre_stats_block(const Params& p, int64_t sx, int64_t nsx, unsigned* s_hist,
                                                 int* s_max) {
-  const int tid = threadIdx.x;
   const int64_t sblk = static_cast<int64_t>(blockIdx.y) * nsx + sx;
   const int64_t total = static_cast<int64_t>(p.pre_views) * p.pre_bpv;
-  for (int64_t i = sblk * kThreads + tid; i < p.pre_zero_words; i += static_cast<int64_t>(gridDim.y) * nsx * kThreads)
-    p.pre_zero[i] = 0u;
   if (sblk < total) {
     const int pv = static_cast<int>(sblk / p.pre_bpv);
     stats_pass(p.pre_stack + pv * p.pre_vs, p.HW, sblk - static_cast<int64_t>(pv) * p.pre_bpv, p.pre_bpv,
@@ -688,6 +584,36 @@ __device__ __forceinline__ Thresholds view_thresholds(const Params& p, int view,
   return thresholds_from_bins(b4, hmax, p.HW, lane);
 }
 
+// Reader `id` of `readers` (ids 0 .. readers - 1, each arriving once) at a
+// two-level arrival counter ctr[0 .. S]: ctr[1 + id % S] counts the readers of
+// its class, the last of each class adds one at ctr[0], and the last of those
+// is the last reader.  (One counter hit by every workgroup of a launch
+// serialises them: k_cloud 33 -> 51 us per c2 step with a single one.)
+template <int S>
+__device__ __forceinline__ bool arrive_last(unsigned* ctr, unsigned id, unsigned readers) {
+  const unsigned cls = id & (S - 1);
+  const unsigned n_cls = (readers - cls + S - 1) / S;  // readers of this class (id < readers)
+  if (atomicAdd(ctr + 1 + cls, 1u) + 1u != n_cls) return false;
+  return atomicAdd(ctr, 1u) + 1u == min(readers, static_cast<unsigned>(S));
+}
+
+// One reader (a whole wave, number id of `readers`) of a view's `words`
+// histogram words at h is done with them: the empty asm consumes values
+// computed from them (the thresholds), so every load has returned before the
+// arrival is counted at h[kSlotArrive ..]; the last reader zeroes the words,
+// the counters included, so the buffer is clean for the next producer
+// whatever launch comes next.
+__device__ __forceinline__ void hist_release(unsigned* h, int words, unsigned id, unsigned readers, int lane,
+                                             uint32_t dep0, uint32_t dep1) {
+  asm volatile("" ::"v"(dep0), "v"(dep1) : "memory");
+  unsigned last = 0u;
+  if (lane == 0) last = arrive_last<8>(h + kSlotArrive, id, readers) ? 1u : 0u;
+  if (__shfl(static_cast<int>(last), 0, 64)) {
+    uint4* h4 = reinterpret_cast<uint4*>(h);
+    for (int i = lane; i < words / 4; i += 64) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 // Mask of 4 packed pixels (one word of white / black bytes): bit e = pixel e
 // has white > tw and white - black > tc (sl_system.py:534-535); byte-SWAR in
 // 16-bit lanes as k_count (tw2 = (tw + 1) * 0x10001, tc2 = (tc + 17) * 0x10001;
@@ -703,30 +629,42 @@ __device__ __forceinline__ uint32_t mask4(uint32_t w, uint32_t b, uint32_t tw2, 
   return (y & 1u) | ((y >> 7) & 2u) | ((y >> 14) & 4u) | ((y >> 21) & 8u);
 }
 
-// k_decode M_DECIDE: the f32 plane table, xn = (u - cx) / fx and yn =
-// (v - cy) / fy in LDS (host: Wp <= kDecPl, W <= kDecX, H <= kDecY; the
-// launch's grid is capped at a few workgroups per CU, so the fill is cheap).
-#ifndef SLGPU_DEC_YN_LDS
-#define SLGPU_DEC_YN_LDS 0
-#endif
-constexpr bool kDecYnLds = SLGPU_DEC_YN_LDS != 0;  // yn in LDS (else one early global load per lane)
-#ifndef SLGPU_DEC_GLDS
-#define SLGPU_DEC_GLDS 1
-#endif
-constexpr bool kDecGlds = SLGPU_DEC_GLDS != 0;  // decision tables by LDS-DMA, overlapping the first stack loads
-#ifndef SLGPU_DEC_PL3
-#define SLGPU_DEC_PL3 0
-#endif
-// (measurement build, SLGPU_DEC_PL3=1: the decision's plane table as packed
-// (n0, n1, n2) floats, 12 B per projector column, Wp <= 1920: 38.4 KB of
-// tables, so that 4 workgroups fit a CU's LDS -- with -DSLGPU_DECODE_WAVES=4
-// -DSLGPU_DECODE_PER_CU=4)
-constexpr bool kDecPl3 = SLGPU_DEC_PL3 != 0;
-constexpr int kDecPl = kDecPl3 ? 1920 : 2048, kDecX = 4096, kDecY = 4096;
-constexpr int kDecPlWords = kDecPl3 ? (kDecPl * 12 + 1023) / 1024 * 256 : kDecPl * 4;  // LDS words of the plane table
-constexpr int kBsSlots = 64;
-constexpr int kSuperCap = 4096;  // super-block sums per launch group (>= sqrt of its blocks)  // k_decode M_DECIDE: chunk-group iterations per workgroup with a barrier-free block sum
-constexpr int kDecodeLds = (kDecPlWords + kDecX + (kDecYnLds ? kDecY : 0)) * 4;  // bytes: > the histogram replicas
+// k_decode M_DECIDE: the f32 plane table and xn = (u - cx) / fx in LDS, by
+// LDS-DMA while the first chunk group's stack loads are in flight (host: Wp <=
+// kDecPl, W <= kDecX, H <= kDecY; the launch's grid is capped at a few
+// workgroups per CU, so the fill is cheap); yn = (v - cy) / fy is one early
+// global load per lane.
+constexpr int kDecPl = 2048, kDecX = 4096, kDecY = 4096;
+constexpr int kDecPlWords = kDecPl * 4;  // LDS words of the plane table
+constexpr int kBsSlots = 64;     // k_decode M_DECIDE: chunk-group iterations per workgroup with a barrier-free block sum
+constexpr int kSuperCap = 4096;  // super-block sums per launch group (>= sqrt of its blocks) + dynamic-grid counters
+constexpr int kSuperWords = 2 * kSuperCap + 4;  // two buffers + their selector words (super_par)
+
+// The super-block buffers alternate from launch group to launch group, and
+// the device, not the host, keeps the alternation: the producer of a group's
+// block sums (k_decode on the decide path, k_count otherwise) reads selector
+// word par[0], accumulates into that buffer, zeroes the other one (its last
+// reader, the previous group's k_cloud, is done) and writes par[1] = its
+// buffer; k_cloud reads par[1] and writes par[0] = the other buffer.  Each
+// word is written only by the kernel that does not read it, so every
+// workgroup of a launch sees one value, and a captured graph replays in any
+// phase (no host state is baked into its launches).  Re-runs
+// (sl_time_kernels) leave both alone.
+__device__ __forceinline__ unsigned* super_produce(const Params& p) {
+  const unsigned sel = p.super_par[0] & 1u;
+  if (!p.rerun && blockIdx.x == 0 && blockIdx.y == 0) {
+    unsigned* other = p.super_base + (sel ^ 1u) * kSuperCap;
+    for (int i = threadIdx.x; i < kSuperCap; i += kThreads) other[i] = 0u;
+    if (threadIdx.x == 0) p.super_par[1] = sel;
+  }
+  return p.super_base + sel * kSuperCap;
+}
+__device__ __forceinline__ const unsigned* super_consume(const Params& p) {
+  const unsigned sel = p.super_par[1] & 1u;
+  if (!p.rerun && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) p.super_par[0] = sel ^ 1u;
+  return p.super_base + sel * kSuperCap;
+}
+constexpr int kDecodeLds = (kDecPlWords + kDecX) * 4;  // bytes: > the histogram replicas
 static_assert(kDecodeLds >= 256 * kHistStride * 4, "the decode LDS holds the histogram replicas too");
 
 // ================================================================ k_decode ====
@@ -735,37 +673,23 @@ static_assert(kDecodeLds >= 256 * kHistStride * 4, "the decode LDS holds the his
 // code of every pixel, reading each plane of the uint8 stack once (M_FROMMAPS:
 // a caller's col_map instead).  Outputs by mode bit:
 //   M_MAPS   col/row int32 maps, full frame, unmasked (what gray_decode
-//            returns), 16-byte stores;
-//   M_CODES  record16 = min(col, Wp-1) (np.clip, sl_system.py:626) per pixel,
-//            for k_count / k_cloud;
-//   M_HIST   the view's black-plane histogram and max(white - black)
-//            (sl_system.py:526-528): LDS replicas bank-skewed so that the
-//            lanes of a half-wave that hit the same bin use 32 different
-//            banks, added to the view's global histogram once per workgroup.
-// Grid (chunk groups, views); waves past the view's last chunk run empty (the
-// workgroup barriers count them).
-#ifndef SLGPU_DECODE_PER_CU
-#define SLGPU_DECODE_PER_CU 3
-#endif
-constexpr int kDecodePerCu = SLGPU_DECODE_PER_CU;  // default k_decode grid cap, workgroups per CU (0: none)
-#ifndef SLGPU_DECODE_WAVES
-#define SLGPU_DECODE_WAVES 3
-#endif
-#ifndef SLGPU_SWAR_GRAY
-#define SLGPU_SWAR_GRAY 1
-#endif
-// Gray bits gathered MSB-first into byte lanes and converted to binary there,
-// 4 pixels per instruction (0: the per-pixel conversion; measurement build)
-constexpr bool kSwarGray = SLGPU_SWAR_GRAY != 0;
-// k_decode's body; group_hook(col, pt, live, n_px, civ, cg, s_lds) runs at
-// the end of each chunk group when the mode has M_FUSED (k_fused: the
-// group's cloud in the same launch), else nothing.
-struct NoGroupHook {
-  template <class... A>
-  __device__ void operator()(A&&...) const {}
-};
-template <int KC, int KR, int MODE, int VEC, class Hook>
-__device__ __forceinline__ void decode_body(const Params& p, const Hook& group_hook) {
+//            returns), 1 KB contiguous per store instruction through an LDS
+//            stage (config 2 120.3-120.6 -> 116.5-117.4 us per step,
+//            profiles/r04_ab/map_stage_lines.jsonl);
+//   M_CODES  the record min(col, Wp-1) (np.clip, sl_system.py:626) per pixel
+//            for k_count / k_cloud (M_DECIDE: 12 bits, 0xfff = no point);
+//   M_HIST   (3-kernel path) the view's black-plane histogram and max(white -
+//            black) (sl_system.py:526-528): LDS replicas bank-skewed so that
+//            the lanes of a half-wave that hit the same bin use 32 different
+//            banks, added to the view's global histogram once per workgroup;
+//   M_DECIDE the mask from k_stats' histograms (or fixed thresholds), the mask
+//            map, the |n.r| > 1e-6 decision, chunk counts and block sums.
+// Grid (chunk groups, views), capped at kDecodePerCu workgroups per CU:
+// chunk groups strided over the grid's x, or (decode_dyn, cloud-only calls)
+// pulled from a per-view counter after the first round.
+constexpr int kDecodePerCu = 3;  // k_decode grid cap, workgroups per CU
+template <int KC, int KR, int MODE, int VEC>
+__global__ __launch_bounds__(kThreads, 3) void k_decode(Params p) {
   const int mode = MODE >= 0 ? MODE : p.mode;
   const int kc = KC >= 0 ? KC : p.kc;
   const int krr = (mode & M_ROWS) ? (KR >= 0 ? KR : p.kr) : 0;
@@ -780,31 +704,22 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
   __shared__ unsigned s_bsum[kBsSlots];  // per iteration: points (low 16 bits) + waves arrived << 16
   __shared__ uint32_t s_thr[2];          // M_DECIDE adaptive: the view's tw2, tc2
   __shared__ unsigned s_mcount;          // M_DECIDE with p.masked: the workgroup's masked pixels
-  // kMapStage: a 1-KB stage per wave for contiguous map stores (maps kernels only)
-  __shared__ uint4 s_mapst[(kMapStage && (MODE < 0 || (MODE & M_MAPS))) ? 64 * kWaves : 1];
+  __shared__ int s_next[2];              // decode_dyn: the workgroup's next chunk group
+  // a 1-KB stage per wave for contiguous map stores (maps kernels only)
+  __shared__ uint4 s_mapst[(MODE < 0 || (MODE & M_MAPS)) ? 64 * kWaves : 1];
   unsigned* s_hist = s_lds;
   float4* s_pl = reinterpret_cast<float4*>(s_lds);
-  const float* s_pl3 = reinterpret_cast<const float*>(s_lds);
   float* s_xn = reinterpret_cast<float*>(s_lds) + kDecPlWords;
-  float* s_yn = s_xn + kDecX;
   const bool decide = (mode & M_DECIDE) != 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
   const int64_t HW = p.HW;
-  // pre-stats workgroups (sl_stack_next, SLGPU_PRE_DECODE=1) after the
-  // decoding ones: the next call's histograms in this launch's tail
-  // (instantiations for calls with a cloud on the decide path only)
-  constexpr bool kPreRole = MODE < 0 || ((MODE & M_DECIDE) && (MODE & M_CODES) && !(MODE & M_FUSED));
-  if (kPreRole && p.decode_gx > 0 && static_cast<int>(blockIdx.x) >= p.decode_gx) {
-    pre_stats_block(p, blockIdx.x - p.decode_gx, gridDim.x - p.decode_gx, s_lds, s_max);
-    return;
-  }
-  const int gx = p.decode_gx > 0 ? p.decode_gx : static_cast<int>(gridDim.x);  // decoding workgroups per view
+  const int gx = static_cast<int>(gridDim.x);  // decoding workgroups per view
   if (decide) {
     if (tid < kBsSlots) s_bsum[tid] = 0u;
-    if (tid == 0) s_mcount = 0u;  // published by the barrier of iteration 0 (or the table fill's)
+    if (tid == 0) s_mcount = 0u;  // published by the barrier of iteration 0
     // the view's mask thresholds (k_stats' histograms), once per workgroup by
     // wave 0 while the others fill the tables: at this point no decode state
     // is live (computed inside the chunk loop they cost registers and ~9 us)
@@ -825,70 +740,38 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
     // the calibration against the frame and Wp <= kDecPl); a maps-only call
     // may run on a context without calibration, or with one for another
     // frame or a wider projector, so it loads none of them.  The fills are
-    // clamped to the LDS the tables own all the same.
-    const bool tables = (mode & M_CODES) != 0;
-    const int wp_t = min(p.Wp, kDecPl), w_t = min(p.W, kDecX);
-    if (tables && kDecGlds) {
-      // the tables by LDS-DMA (16 B per lane, 1 KB per wave instruction): no
-      // VGPRs, and the first chunk group's stack loads below are issued
-      // while they land; the workgroup barrier before the first mask
-      // (iteration 0) publishes them.  Lanes past the end repeat the last
-      // entry into slack LDS (kDecPl, kDecX are multiples of 64 entries).
+    // clamped to the LDS the tables own all the same.  By LDS-DMA (16 B per
+    // lane, 1 KB per wave instruction): no VGPRs, and the first chunk group's
+    // stack loads below are issued while they land; the workgroup barrier
+    // before the first mask (iteration 0) publishes them.  Lanes past the end
+    // repeat the last entry into slack LDS (kDecPl, kDecX are multiples of 64
+    // entries).
+    if (mode & M_CODES) {
+      const int wp_t = min(p.Wp, kDecPl), w_t = min(p.W, kDecX);
       typedef __attribute__((address_space(3))) void* lds_ptr_t;
-      if (kDecPl3) {  // the packed 12-B table as bytes, 1 KB per wave instruction (slack: kDecPlWords)
-        const uint8_t* src = reinterpret_cast<const uint8_t*>(p.planes12);
-        for (int i = wid; i * 1024 < wp_t * 12; i += kWaves)
-          __builtin_amdgcn_global_load_lds(src + 16 * (i * 64 + lane), (lds_ptr_t)(s_lds + i * 256), 16, 0, 0);
-      } else {
-        for (int i = wid; i * 64 < wp_t; i += kWaves)
-          __builtin_amdgcn_global_load_lds(p.planes32 + min(i * 64 + lane, wp_t - 1), (lds_ptr_t)(s_pl + i * 64), 16, 0, 0);
-      }
+      for (int i = wid; i * 64 < wp_t; i += kWaves)
+        __builtin_amdgcn_global_load_lds(p.planes32 + min(i * 64 + lane, wp_t - 1), (lds_ptr_t)(s_pl + i * 64), 16, 0, 0);
       for (int i = wid; i * 256 < w_t; i += kWaves)
         __builtin_amdgcn_global_load_lds(p.xn32 + min(i * 256 + 4 * lane, w_t - 4), (lds_ptr_t)(s_xn + i * 256), 16, 0, 0);
-    } else if (tables) {
-      for (int i = tid; i < wp_t; i += kThreads) {
-        if (kDecPl3) {
-          float* d = reinterpret_cast<float*>(s_lds) + 3 * i;
-          d[0] = p.planes12[3 * i];
-          d[1] = p.planes12[3 * i + 1];
-          d[2] = p.planes12[3 * i + 2];
-        } else {
-          s_pl[i] = p.planes32[i];
-        }
-      }
-      for (int i = tid; i < w_t; i += kThreads) s_xn[i] = p.xn32[i];
     }
-    if (tables && kDecYnLds)
-      for (int i = tid; i < min(p.H, kDecY); i += kThreads) s_yn[i] = p.yn32[i];
-    if (!kDecGlds) __syncthreads();
   }
   uint32_t tw2 = static_cast<uint32_t>(40 + 1) * 0x00010001u;      // fixed mask:
   uint32_t tc2 = static_cast<uint32_t>(10 + 17) * 0x00010001u;     // multi_point_cloud_process.py:36-38
-  if (!kDecGlds && decide && (mode & M_HIST)) {  // adaptive: the view's (wave 0 above; the table fill's barrier)
-    tw2 = __builtin_amdgcn_readfirstlane(s_thr[0]);
-    tc2 = __builtin_amdgcn_readfirstlane(s_thr[1]);
-  }
   int it = 0;
 
-  // the next launch's super-block sums (scratch of this one)
-  if (p.super_zero && blockIdx.x == 0 && blockIdx.y == 0)
-    for (int i = tid; i < p.super_cap; i += kThreads) p.super_zero[i] = 0u;
-  // the next launch's histogram (scratch of this one)
-  if (hist && blockIdx.x == 0)
-    for (int i = tid; i < kSlot; i += kThreads) p.hist_zero[view * kSlot + i] = 0u;
   if (hist) {
     for (int i = tid; i < 256 * kHistStride; i += kThreads) s_hist[i] = 0u;
     __syncthreads();
   }
 
-  // Chunk groups of the view, strided over the grid's x (one group per
-  // workgroup unless the launch caps the grid, SLGPU_DECODE_GRID); the
-  // workgroup-uniform loop holds no barrier.
+  // Chunk groups of the view, strided over the grid's x (or pulled
+  // dynamically); the workgroup-uniform loop holds no barrier but the
+  // first iteration's (M_DECIDE) and the block sums' (unless bs_atomic).
   const int ngroups = (p.cpv + kWaves - 1) / kWaves;
   int mx_acc = -1024;
-  __shared__ int s_next[2];  // decode_dyn: the workgroup's next chunk group
-  const bool dyn = p.decode_dyn && decide && (mode & M_CODES) && !(mode & M_FUSED) && !p.bs_atomic;
-  unsigned* const dyn_ctr = p.super_sums + (p.super_cap - 1 - view);
+  const bool dyn = p.decode_dyn && decide && (mode & M_CODES) && !p.bs_atomic;
+  unsigned* const sup = (decide && (mode & M_CODES)) ? super_produce(p) : nullptr;
+  unsigned* const dyn_ctr = sup + (kSuperCap - 1 - view);
   for (int cg = blockIdx.x; cg < ngroups;) {
   // decode_dyn: this workgroup's claim on a later chunk group, issued now so
   // that its round trip overlaps this group's loads (published below)
@@ -901,12 +784,17 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
   const int64_t pxl = n_px > 0 ? px0 : 0;  // keep loads unconditional and in bounds
   const int64_t o = view * HW + px0;
 
-  // M_DECIDE without yn in LDS: the row's yn first (the oldest load: waiting
-  // for it never waits for this iteration's stores)
-  const float ys_early = (decide && !kDecYnLds && (mode & M_CODES) && n_px > 0)
-                             ? p.yn32[row_of(p, static_cast<int>(px0))] : 0.0f;
+  // M_DECIDE: the row's yn first (the oldest load: waiting for it never
+  // waits for this iteration's stores)
+  const float ys_early = (decide && (mode & M_CODES) && n_px > 0) ? p.yn32[row_of(p, static_cast<int>(px0))] : 0.0f;
   uint32_t col[kPx];
   uint32_t pt_rec = 0xffffu;  // the lane's point bits for 12-bit records (decide path)
+  uint4 wq = make_uint4(0u, 0u, 0u, 0u), bq = wq;
+  // binary code words per byte lane (pixel 4 w + e in byte 3 - e): a code's
+  // top min(k, 8) bits in A, the rest in B
+  uint32_t rA[4] = {0, 0, 0, 0}, rB[4] = {0, 0, 0, 0};
+  const int rBn = krr > 8 ? krr - 8 : 0;
+  const int rSh = nr - krr;
   if (mode & M_FROMMAPS) {
     // reconstruct_point_cloud's input col_map (clipped below, sl_system.py:626)
     const int64_t ol = view * HW + pxl;
@@ -947,54 +835,31 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
       }
       return ld16(vbase + pxl + static_cast<int64_t>(plane) * HW, n_px, false);
     };
-    const uint4 wq = ldp(0);
-    const uint4 bq = ldp(1);
+    wq = ldp(0);
+    bq = ldp(1);
     // ---- Gray bit planes: (pattern, inverse) pairs, columns then rows ----
+    // Each (pattern, inverse) compare is one v_bitop3 per word; the bit enters
+    // at bit 7 of its byte lane and the lane shifts right, acc = (acc >> 1 &
+    // 0x7f..) | (bit7 & 0x80..): at most 8 bits per byte lane, so no carry
+    // crosses into the neighbouring pixel; codes of up to 16 bits use A then
+    // B.  The first pair ends lowest, bit-reversed below.
     const int npl = 2 * (kc + krr);
     uint32_t cA[4] = {0, 0, 0, 0}, cB[4] = {0, 0, 0, 0};
-    uint32_t rA[4] = {0, 0, 0, 0}, rB[4] = {0, 0, 0, 0};
-    // Fold one (pattern, inverse) pair into per-byte-lane accumulators:
-    // acc = (acc << 1) | bit holds at most 8 bits per byte lane, so no carry
-    // crosses into the neighbouring pixel; codes of up to 16 bits use A then B.
-    // (kSwarGray: each bit enters at bit 7 of its byte lane and the lane
-    // shifts right, acc = (acc >> 1 & 0x7f..) | (bit7 & 0x80..): the first
-    // pair ends lowest, bit-reversed below; 6 instructions per word and pair)
     auto consume = [&](const uint4& P, const uint4& I, int pair) {
-      if (kSwarGray) {
-        auto ins = [](uint32_t acc, uint32_t g) { return ((acc >> 1) & 0x7f7f7f7fu) | (g & 0x80808080u); };
-        uint32_t g[4];
+      auto ins = [](uint32_t acc, uint32_t g) { return ((acc >> 1) & 0x7f7f7f7fu) | (g & 0x80808080u); };
+      uint32_t g[4];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) g[w] = gt_bit7(word(P, w), word(I, w));
+      for (int w = 0; w < 4; ++w) g[w] = gt_bit7(word(P, w), word(I, w));
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          if (pair < kc) {
-            if (pair < 8) cA[w] = ins(cA[w], g[w]);
-            else cB[w] = ins(cB[w], g[w]);
-          } else if (pair - kc < 8) {
-            rA[w] = ins(rA[w], g[w]);
-          } else {
-            rB[w] = ins(rB[w], g[w]);
-          }
-        }
-        return;
-      }
-      uint32_t m[4];
-#pragma unroll
-      for (int w = 0; w < 4; ++w) m[w] = gt_msb(word(P, w), word(I, w)) >> 7;
-      if (pair < kc) {
-        if (pair < 8) {
-#pragma unroll
-          for (int w = 0; w < 4; ++w) cA[w] = (cA[w] << 1) | m[w];
+      for (int w = 0; w < 4; ++w) {
+        if (pair < kc) {
+          if (pair < 8) cA[w] = ins(cA[w], g[w]);
+          else cB[w] = ins(cB[w], g[w]);
+        } else if (pair - kc < 8) {
+          rA[w] = ins(rA[w], g[w]);
         } else {
-#pragma unroll
-          for (int w = 0; w < 4; ++w) cB[w] = (cB[w] << 1) | m[w];
+          rB[w] = ins(rB[w], g[w]);
         }
-      } else if (pair - kc < 8) {
-#pragma unroll
-        for (int w = 0; w < 4; ++w) rA[w] = (rA[w] << 1) | m[w];
-      } else {
-#pragma unroll
-        for (int w = 0; w < 4; ++w) rB[w] = (rB[w] << 1) | m[w];
       }
     };
     if (KC >= 0) {
@@ -1039,285 +904,208 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
         }
       }
     }
-    // ---- Gray -> binary ----
-    const int cBn = kc > 8 ? kc - 8 : 0;
-    const int rBn = krr > 8 ? krr - 8 : 0;
-    const int cSh = nc - kc;
-    const int rSh = nr - krr;
-    uint32_t row[kPx];
-    if (kSwarGray) {
-      // A code's top min(k, 8) Gray bits are in A, the rest in B, each
-      // bit-reversed by the right-shifting accumulators: bitreverse puts them
-      // MSB-first in the low bits of each byte (pixel 4 w + e in byte 3 - e).
-      // Binary per byte lane; B's bits continue A's prefix xor, so A's binary
-      // lowest bit (the parity of its Gray bits) is xor-ed into B's top bit
-      // before B's own conversion.
-      // Codes shifted by sh = n - k bits (fewer patterns than code bits):
-      // binary(g << sh) = binary(g) << sh with its lowest bit repeated below.
-      auto to_binary = [](uint32_t (&A)[4], uint32_t (&B)[4], int k) {
-        const int kA = k < 8 ? k : 8, kB = k - kA;
+    // ---- Gray -> binary in the byte lanes, 4 pixels per instruction ----
+    // bitreverse puts each byte lane's bits MSB-first in its low bits (pixel
+    // 4 w + e in byte 3 - e); B's bits continue A's prefix xor, so A's binary
+    // lowest bit (the parity of its Gray bits) is xor-ed into B's top bit
+    // before B's own conversion.  Codes shifted by sh = n - k bits (fewer
+    // patterns than code bits): binary(g << sh) = binary(g) << sh with its
+    // lowest bit repeated below.
+    auto to_binary = [](uint32_t (&A)[4], uint32_t (&B)[4], int k) {
+      const int kA = k < 8 ? k : 8, kB = k - kA;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          A[w] = gray_to_binary_bytes(__builtin_bitreverse32(A[w]), kA);
-          // (A's parity flips B's top bit: every bit below it follows)
-          B[w] = kB > 0 ? gray_to_binary_bytes(__builtin_bitreverse32(B[w]) ^ ((A[w] & 0x01010101u) << (kB - 1)), kB)
-                        : 0u;
-        }
-      };
-      to_binary(cA, cB, kc);
+      for (int w = 0; w < 4; ++w) {
+        A[w] = gray_to_binary_bytes(__builtin_bitreverse32(A[w]), kA);
+        B[w] = kB > 0 ? gray_to_binary_bytes(__builtin_bitreverse32(B[w]) ^ ((A[w] & 0x01010101u) << (kB - 1)), kB)
+                      : 0u;
+      }
+    };
+    const int cBn = kc > 8 ? kc - 8 : 0;
+    const int cSh = nc - kc;
+    to_binary(cA, cB, kc);
+#pragma unroll
+    for (int q = 0; q < kPx; ++q) {
+      const int w = q >> 2, sft = 8 * (3 - (q & 3));
+      col[q] = (((cA[w] >> sft) & 0xffu) << cBn) | ((cB[w] >> sft) & 0xffu);
+    }
+    if (cSh > 0) {
 #pragma unroll
       for (int q = 0; q < kPx; ++q) {
-        const int w = q >> 2, sft = 8 * (3 - (q & 3));
-        col[q] = (((cA[w] >> sft) & 0xffu) << cBn) | ((cB[w] >> sft) & 0xffu);
-      }
-      if (cSh > 0) {
-#pragma unroll
-        for (int q = 0; q < kPx; ++q) {
-          const uint32_t lo = col[q] & 1u;
-          col[q] = (col[q] << cSh) | ((lo << cSh) - lo);
-        }
-      }
-      // rows: only the maps store reads them -- converted there, a word at a time
-      if (mode & M_ROWS) to_binary(rA, rB, krr);
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) row[k] = 0u;
-    } else {
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) {
-        const int w = k >> 2, sft = 8 * (k & 3);
-        const uint32_t gc = (((cA[w] >> sft) & 0xffu) << cBn) | ((cB[w] >> sft) & 0xffu);
-        const uint32_t gr = (((rA[w] >> sft) & 0xffu) << rBn) | ((rB[w] >> sft) & 0xffu);
-        col[k] = gray_to_binary(gc << cSh);
-        row[k] = (mode & M_ROWS) ? gray_to_binary(gr << rSh) : 0u;
+        const uint32_t lo = col[q] & 1u;
+        col[q] = (col[q] << cSh) | ((lo << cSh) - lo);
       }
     }
-    // (kSwarGray) pixel 4 w + e's row code from the binary row words
-    auto row_code = [&](int w, int e) -> uint32_t {
-      const int sft = 8 * (3 - e);
-      uint32_t v = (((rA[w] >> sft) & 0xffu) << rBn) | ((rB[w] >> sft) & 0xffu);
-      if (rSh > 0) {
-        const uint32_t lo = v & 1u;
-        v = (v << rSh) | ((lo << rSh) - lo);
-      }
-      return v;
-    };
-    if (mode & M_MAPS) {
-      if (vec) {
-        if (n_px == kPx && kMapAux) {
-          const int64_t vb = view * HW;  // (4 HW < 2^31: measurement builds only)
-          const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(p.col_out + vb, 0, static_cast<int>(4 * HW), 0x00020000);
-          const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(p.row_out + vb, 0, static_cast<int>(4 * HW), 0x00020000);
-          const int bo = 4 * static_cast<int>(px0);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            __builtin_amdgcn_raw_buffer_store_b128(v4u{col[4 * i], col[4 * i + 1], col[4 * i + 2], col[4 * i + 3]}, rc,
-                                                   bo + 16 * i, 0, kMapAux);
-            uint32_t r4[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) r4[e] = kSwarGray ? row_code(i, e) : row[4 * i + e];
-            __builtin_amdgcn_raw_buffer_store_b128(v4u{r4[0], r4[1], r4[2], r4[3]}, rr, bo + 16 * i, 0, kMapAux);
-          }
-        } else if (kMapStage && live) {
-          // 1-KB contiguous map stores through a 1-KB LDS stage per wave:
-          // for each quarter j of the chunk (pixels 256 j .. 256 j + 255, the
-          // 16 lanes of DPP row j), those lanes put their 64 B in the stage,
-          // then lane l stores bytes 16 l .. 16 l + 15 of it (pixels
-          // 256 j + 4 l ..); a lane stores only where its source lane's 16
-          // pixels are in the view (whole 16-pixel groups: W % 16 == 0)
-          uint4* const stg = s_mapst + 64 * wid;
-          const int64_t cbase = view * HW + static_cast<int64_t>(civ) * kChunk;  // the chunk's first pixel
-#pragma unroll
-          for (int m = 0; m < 2; ++m) {
-            if (m == 1 && SLGPU_MAP_STAGE == 1) {  // (1: the col map only; the rows as below)
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                uint32_t r4[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) r4[e] = kSwarGray ? row_code(i, e) : row[4 * i + e];
-                if (n_px == kPx) st_map(p.row_out + o + 4 * i, r4[0], r4[1], r4[2], r4[3]);
-              }
-              continue;
-            }
-            // the chunk's 4 KB of this map as a buffer (SGPRs): stores past the
-            // view's end (its last, partial chunk) fall outside it and are dropped
-            const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-                (m == 0 ? p.col_out : p.row_out) + cbase, 0,
-                static_cast<int>(4 * min<int64_t>(kChunk, HW - static_cast<int64_t>(civ) * kChunk)), 0x00020000);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              if ((lane >> 4) == j && n_px == kPx) {
-                const int u = lane & 15;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                  uint32_t v4[4];
-#pragma unroll
-                  for (int e = 0; e < 4; ++e)
-                    v4[e] = m == 0 ? col[4 * q + e] : (kSwarGray ? row_code(q, e) : row[4 * q + e]);
-                  stg[4 * u + q] = make_uint4(v4[0], v4[1], v4[2], v4[3]);
-                }
-              }
-              __builtin_amdgcn_wave_barrier();
-              const uint4 v = stg[lane];
-              __builtin_amdgcn_wave_barrier();
-              __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rd, 1024 * j + 16 * lane, 0, 0);
-            }
-          }
-        } else if (n_px == kPx) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            st_map(p.col_out + o + 4 * i, col[4 * i], col[4 * i + 1], col[4 * i + 2], col[4 * i + 3]);
-            if (kSwarGray) {
-              uint32_t r4[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) r4[e] = row_code(i, e);
-              st_map(p.row_out + o + 4 * i, r4[0], r4[1], r4[2], r4[3]);
-            } else {
-              st_map(p.row_out + o + 4 * i, row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < kPx; ++k) {
-          if (k < n_px) {
-            p.col_out[o + k] = static_cast<int32_t>(col[k]);
-            p.row_out[o + k] = static_cast<int32_t>(kSwarGray ? row_code(k >> 2, k & 3) : row[k]);
-          }
-        }
-      }
+    // rows: only the maps store reads them -- converted there, a word at a time
+    if (mode & M_ROWS) to_binary(rA, rB, krr);
+  }
+  // pixel 4 w + e's row code from the binary row words
+  auto row_code = [&](int w, int e) -> uint32_t {
+    const int sft = 8 * (3 - e);
+    uint32_t v = (((rA[w] >> sft) & 0xffu) << rBn) | ((rB[w] >> sft) & 0xffu);
+    if (rSh > 0) {
+      const uint32_t lo = v & 1u;
+      v = (v << rSh) | ((lo << rSh) - lo);
     }
-    if (decide) {
-      if (kDecGlds && it == 0) {  // workgroup-uniform: the LDS-DMA tables and s_thr are in
-        __syncthreads();
-        if (mode & M_HIST) {
-          tw2 = __builtin_amdgcn_readfirstlane(s_thr[0]);
-          tc2 = __builtin_amdgcn_readfirstlane(s_thr[1]);
-        }
-      }
-      // ---- mask with the view's thresholds (tw2 / tc2: computed at kernel start) ----
-      uint32_t ok = 0u, mb[4];
+    return v;
+  };
+  if (mode & M_MAPS) {
+    if (vec && live) {
+      // For each quarter j of the chunk (pixels 256 j .. 256 j + 255, the 16
+      // lanes of DPP row j), those lanes put their 64 B in the wave's stage,
+      // then lane l stores bytes 16 l .. 16 l + 15 of it (pixels 256 j + 4 l
+      // ..): 1 KB contiguous per instruction.  A lane writes the stage only
+      // where its 16 pixels are in the view (whole 16-pixel groups: W % 16 ==
+      // 0), and the chunk's buffer descriptor drops stores past the view's end.
+      uint4* const stg = s_mapst + 64 * wid;
+      const int64_t cbase = view * HW + static_cast<int64_t>(civ) * kChunk;  // the chunk's first pixel
 #pragma unroll
-      for (int w = 0; w < 4; ++w) ok |= mask4(word(wq, w), word(bq, w), tw2, tc2, &mb[w]) << (4 * w);
-      if (n_px != kPx) ok = 0u;  // vec: whole 16-pixel groups
-      if (p.masked) {  // (uniform) the chunk's masked pixels into the workgroup's count
-        const int mc = wave_sum_dpp(__popc(ok));
-        if (lane == 0 && mc) atomicAdd(&s_mcount, static_cast<unsigned>(mc));
-      }
-      if ((mode & M_MAPS) && n_px == kPx) {
-        if (kMapAux) {
-          const __amdgpu_buffer_rsrc_t rm =
-              __builtin_amdgcn_make_buffer_rsrc(p.mask_out + view * HW, 0, static_cast<int>(HW), 0x00020000);
-          __builtin_amdgcn_raw_buffer_store_b128(v4u{mb[0], mb[1], mb[2], mb[3]}, rm, static_cast<int>(px0), 0, kMapAux);
-        } else {
-          *reinterpret_cast<uint4*>(p.mask_out + o) = make_uint4(mb[0], mb[1], mb[2], mb[3]);
-        }
-      }
-      // ---- |n.r| > 1e-6 (sl_system.py:638-642) of the masked pixels, LDS tables ----
-      uint32_t pt = 0u;
-      if ((mode & M_CODES) && ok) {
-        const int px0i = static_cast<int>(px0);
-        const int v = row_of(p, px0i), u0 = px0i - v * p.W;  // the lane's 16 pixels share row v (W % 16 == 0)
-        float4 pf[kPx];
+      for (int m = 0; m < 2; ++m) {
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            (m == 0 ? p.col_out : p.row_out) + cbase, 0,
+            static_cast<int>(4 * min<int64_t>(kChunk, HW - static_cast<int64_t>(civ) * kChunk)), 0x00020000);
 #pragma unroll
-        for (int k = 0; k < kPx; ++k) {
-          const uint32_t ck = min(col[k], static_cast<uint32_t>(p.Wp - 1));
-          pf[k] = kDecPl3 ? make_float4(s_pl3[3 * ck], s_pl3[3 * ck + 1], s_pl3[3 * ck + 2], 0.0f) : s_pl[ck];
-        }
-        float xs[kPx];
+        for (int j = 0; j < 4; ++j) {
+          if ((lane >> 4) == j && n_px == kPx) {
+            const int u = lane & 15;
 #pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const float4 x4 = reinterpret_cast<const float4*>(s_xn + u0)[q4];
-          xs[4 * q4] = x4.x;
-          xs[4 * q4 + 1] = x4.y;
-          xs[4 * q4 + 2] = x4.z;
-          xs[4 * q4 + 3] = x4.w;
-        }
-        const float ys = kDecYnLds ? s_yn[v] : ys_early;
-        uint32_t todo = ok;
-        if (!(mode & M_NC)) {  // k_count's one-compare sufficient test (p.fast_thr, sl_set_calib)
+            for (int q = 0; q < 4; ++q) {
+              uint32_t v4[4];
 #pragma unroll
-          for (int k = 0; k < kPx; ++k) {
-            const float a = fabsf(__builtin_fmaf(pf[k].x, xs[k], __builtin_fmaf(pf[k].y, ys, pf[k].z)));
-            if (a > p.fast_thr) pt |= 1u << k;
-          }
-          pt &= ok;
-          todo &= ~pt;
-        }
-#pragma unroll
-        for (int k = 0; k < kPx; ++k) {  // the bounded f32 test, f64 where undecided
-          if (!((todo >> k) & 1u)) continue;
-          const int c = static_cast<int>(min(col[k], static_cast<uint32_t>(p.Wp - 1)));
-          const int64_t q = px0 + k;
-          float x, y, z, inv;
-          if (mode & M_NC) {
-            x = static_cast<float>(p.nc_rays[q]);
-            y = static_cast<float>(p.nc_rays[HW + q]);
-            z = static_cast<float>(p.nc_rays[2 * HW + q]);
-            inv = 1.0f;
-          } else {
-            x = xs[k];
-            y = ys;
-            z = 1.0f;
-            inv = __frsqrt_rn(x * x + y * y + 1.0f);
-          }
-          if (has_point(p, mode, pf[k], c, x, y, z, inv, u0 + k, v, q)) pt |= 1u << k;
-        }
-      }
-      if (mode & M_CODES) {
-        // point nibbles in k_count's layout (byte 64 s + l: pixels 256 s + 4 l + e):
-        // this lane's 16 pixels are the 4 bytes at 4 lane
-        const int64_t gci = static_cast<int64_t>(view) * p.cpv + civ;
-        pt_rec = pt;
-        if (live && !p.rec12) {  // (12-bit records carry the point bits: code 0xfff = no point)
-          const uint32_t nw = (pt & 0xfu) | ((pt & 0xf0u) << 4) | ((pt & 0xf00u) << 8) | ((pt & 0xf000u) << 12);
-          *reinterpret_cast<uint32_t*>(p.ptnib + gci * kChunkNib + 4 * lane) = nw;
-        }
-        const int cnt = wave_sum_dpp(__popc(pt));
-        if (lane == 0) {
-          if (live) p.chunk_counts[gci] = cnt;
-          const unsigned mine = live ? static_cast<unsigned>(cnt) : 0u;
-          if (p.bs_atomic) {
-            // the workgroup's block sum without a barrier: the last of its
-            // waves to add its count (one LDS slot per iteration) writes it
-            const unsigned old = atomicAdd(&s_bsum[it], (1u << 16) | mine);
-            if ((old >> 16) == kWaves - 1) {
-              const int64_t blk = static_cast<int64_t>(view) * ngroups + cg;
-              const unsigned t = (old & 0xffffu) + mine;
-              p.block_sums[blk] = static_cast<int>(t);
-              if (t) atomicAdd(p.super_sums + (blk >> p.sb_shift), t);
+              for (int e = 0; e < 4; ++e) v4[e] = m == 0 ? col[4 * q + e] : row_code(q, e);
+              stg[4 * u + q] = make_uint4(v4[0], v4[1], v4[2], v4[3]);
             }
-          } else {
-            s_cnt[it & 1][wid] = static_cast<int>(mine);
           }
+          __builtin_amdgcn_wave_barrier();
+          const uint4 v = stg[lane];
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rd, 1024 * j + 16 * lane, 0, 0);
         }
       }
-    }
-    if (hist) {
-      unsigned* hrow = s_hist + (lane & (kHistRep - 1));
-      int mx = -1024;
+    } else if (!vec) {
 #pragma unroll
       for (int k = 0; k < kPx; ++k) {
         if (k < n_px) {
-          const int bk = static_cast<int>(byte_of(bq, k));
-          atomicAdd(hrow + bk * kHistStride, 1u);
-          mx = max(mx, static_cast<int>(byte_of(wq, k)) - bk);
+          p.col_out[o + k] = static_cast<int32_t>(col[k]);
+          p.row_out[o + k] = static_cast<int32_t>(row_code(k >> 2, k & 3));
         }
       }
-      mx_acc = max(mx_acc, mx);
     }
   }
+  if (decide) {
+    if (it == 0) {  // workgroup-uniform: the LDS-DMA tables and s_thr are in
+      __syncthreads();
+      if (mode & M_HIST) {
+        tw2 = __builtin_amdgcn_readfirstlane(s_thr[0]);
+        tc2 = __builtin_amdgcn_readfirstlane(s_thr[1]);
+      }
+    }
+    // ---- mask with the view's thresholds ----
+    uint32_t ok = 0u, mb[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) ok |= mask4(word(wq, w), word(bq, w), tw2, tc2, &mb[w]) << (4 * w);
+    if (n_px != kPx) ok = 0u;  // vec: whole 16-pixel groups
+    if (p.masked) {  // (uniform) the chunk's masked pixels into the workgroup's count
+      const int mc = wave_sum_dpp(__popc(ok));
+      if (lane == 0 && mc) atomicAdd(&s_mcount, static_cast<unsigned>(mc));
+    }
+    if ((mode & M_MAPS) && n_px == kPx) *reinterpret_cast<uint4*>(p.mask_out + o) = make_uint4(mb[0], mb[1], mb[2], mb[3]);
+    // ---- |n.r| > 1e-6 (sl_system.py:638-642) of the masked pixels, LDS tables ----
+    uint32_t pt = 0u;
+    if ((mode & M_CODES) && ok) {
+      const int px0i = static_cast<int>(px0);
+      const int v = row_of(p, px0i), u0 = px0i - v * p.W;  // the lane's 16 pixels share row v (W % 16 == 0)
+      float4 pf[kPx];
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) pf[k] = s_pl[min(col[k], static_cast<uint32_t>(p.Wp - 1))];
+      float xs[kPx];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const float4 x4 = reinterpret_cast<const float4*>(s_xn + u0)[q4];
+        xs[4 * q4] = x4.x;
+        xs[4 * q4 + 1] = x4.y;
+        xs[4 * q4 + 2] = x4.z;
+        xs[4 * q4 + 3] = x4.w;
+      }
+      const float ys = ys_early;
+      uint32_t todo = ok;
+      if (!(mode & M_NC)) {  // k_count's one-compare sufficient test (p.fast_thr, sl_set_calib)
+#pragma unroll
+        for (int k = 0; k < kPx; ++k) {
+          const float a = fabsf(__builtin_fmaf(pf[k].x, xs[k], __builtin_fmaf(pf[k].y, ys, pf[k].z)));
+          if (a > p.fast_thr) pt |= 1u << k;
+        }
+        pt &= ok;
+        todo &= ~pt;
+      }
+#pragma unroll
+      for (int k = 0; k < kPx; ++k) {  // the bounded f32 test, f64 where undecided
+        if (!((todo >> k) & 1u)) continue;
+        const int c = static_cast<int>(min(col[k], static_cast<uint32_t>(p.Wp - 1)));
+        const int64_t q = px0 + k;
+        float x, y, z, inv;
+        if (mode & M_NC) {
+          x = static_cast<float>(p.nc_rays[q]);
+          y = static_cast<float>(p.nc_rays[HW + q]);
+          z = static_cast<float>(p.nc_rays[2 * HW + q]);
+          inv = 1.0f;
+        } else {
+          x = xs[k];
+          y = ys;
+          z = 1.0f;
+          inv = __frsqrt_rn(x * x + y * y + 1.0f);
+        }
+        if (has_point(p, mode, pf[k], c, x, y, z, inv, u0 + k, v, q)) pt |= 1u << k;
+      }
+    }
+    if (mode & M_CODES) {
+      const int64_t gci = static_cast<int64_t>(view) * p.cpv + civ;
+      pt_rec = pt;  // (the 12-bit records carry the point bits: code 0xfff = no point)
+      const int cnt = wave_sum_dpp(__popc(pt));
+      if (lane == 0) {
+        if (live) p.chunk_counts[gci] = cnt;
+        const unsigned mine = live ? static_cast<unsigned>(cnt) : 0u;
+        if (p.bs_atomic) {
+          // the workgroup's block sum without a barrier: the last of its
+          // waves to add its count (one LDS slot per iteration) writes it
+          const unsigned old = atomicAdd(&s_bsum[it], (1u << 16) | mine);
+          if ((old >> 16) == kWaves - 1) {
+            const int64_t blk = static_cast<int64_t>(view) * ngroups + cg;
+            const unsigned t = (old & 0xffffu) + mine;
+            p.block_sums[blk] = static_cast<int>(t);
+            if (t) atomicAdd(sup + (blk >> p.sb_shift), t);
+          }
+        } else {
+          s_cnt[it & 1][wid] = static_cast<int>(mine);
+        }
+      }
+    }
+  }
+  if (hist) {
+    unsigned* hrow = s_hist + (lane & (kHistRep - 1));
+    int mx = -1024;
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      if (k < n_px) {
+        const int bk = static_cast<int>(byte_of(bq, k));
+        atomicAdd(hrow + bk * kHistStride, 1u);
+        mx = max(mx, static_cast<int>(byte_of(wq, k)) - bk);
+      }
+    }
+    mx_acc = max(mx_acc, mx);
+  }
 
-  if ((mode & M_CODES) && !p.rec_col && !(mode & M_FUSED)) {
+  if (mode & M_CODES) {
     // records for k_count / k_cloud: clipped column code
     uint32_t rec[kPx / 2];
 #pragma unroll
     for (int i = 0; i < kPx / 2; ++i)
       rec[i] = min(col[2 * i], static_cast<uint32_t>(p.Wp - 1)) |
                (min(col[2 * i + 1], static_cast<uint32_t>(p.Wp - 1)) << 16);
-    if (vec && p.rec12) {
-      // (chunk slots without maps: the maps kernels keep the pixel order, whose
-      // registers fit; the host sets p.rec_blk to match, for k_cloud)
-      const bool blk = kRecBlk && (!(mode & M_MAPS) || SLGPU_REC_BLK_MAPS);
+    if (decide) {
+      // 12-bit records (M_DECIDE implies the vector path and Wp <= 2048):
+      // chunk slots without maps, pixel order with them (the host sets
+      // p.rec_blk to match, for k_cloud)
+      const bool blk = !(mode & M_MAPS);
       if (n_px == kPx) {  // 8 codes per 3 words
         uint32_t rw[6];
         uint32_t* ro = blk ? rw : reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p.codes) + 3 * o / 2);
@@ -1351,7 +1139,7 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
         if (k < n_px) p.codes[o + k] = static_cast<uint16_t>(rec[k >> 1] >> (16 * (k & 1)));
     }
   }
-  if (decide && (mode & M_CODES) && !p.bs_atomic && !(mode & M_FUSED)) {  // the workgroup's block sum (k_count's, for k_cloud's offsets)
+  if (decide && (mode & M_CODES) && !p.bs_atomic) {  // the workgroup's block sum (k_count's, for k_cloud's offsets)
     if (dyn && tid == 0) s_next[it & 1] = static_cast<int>(dyn_next) + gx;
     __syncthreads();
     if (tid == 0) {
@@ -1360,10 +1148,9 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
       for (int w = 0; w < kWaves; ++w) t += s_cnt[it & 1][w];
       const int64_t blk = static_cast<int64_t>(view) * ngroups + cg;
       p.block_sums[blk] = t;
-      if (t) atomicAdd(p.super_sums + (blk >> p.sb_shift), static_cast<unsigned>(t));
+      if (t) atomicAdd(sup + (blk >> p.sb_shift), static_cast<unsigned>(t));
     }
   }
-  if (mode & M_FUSED) group_hook(col, pt_rec, live, n_px, civ, cg, s_lds);
   cg = dyn ? s_next[it & 1] : cg + gx;  // (dyn: published before the block-sum barrier above)
   ++it;
   }  // chunk groups
@@ -1372,6 +1159,11 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
     __syncthreads();
     if (tid == 0 && s_mcount) atomicAdd(p.masked + view, static_cast<unsigned long long>(s_mcount));
   }
+  // the last of the view's workgroups to have read its histograms zeroes them
+  // (here at the end: wave 0 waiting on the arrival atomic at the start delayed
+  // its first stack loads, k_decode +3 us per c2 step; tw2 / tc2 came from them)
+  if (decide && (mode & M_HIST) && !p.rerun && wid == 0)
+    hist_release(p.hist + static_cast<int64_t>(view) * kHistView, kHistView, blockIdx.x, gx, lane, tw2, tc2);
 
   if (hist) {
 #pragma unroll
@@ -1391,11 +1183,6 @@ __device__ __forceinline__ void decode_body(const Params& p, const Hook& group_h
       if (m > -1024) atomicMax(gh + 256, static_cast<unsigned>(m + 1024));
     }
   }
-}
-
-template <int KC, int KR, int MODE, int VEC>
-__global__ __launch_bounds__(kThreads, SLGPU_DECODE_WAVES) void k_decode(Params p) {
-  decode_body<KC, KR, MODE, VEC>(p, NoGroupHook{});
 }
 
 // ================================================================= k_count ====
@@ -1426,7 +1213,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
   // scan then waits for it alone), then the chunk ----
   uint4 hb = make_uint4(0u, 0u, 0u, 0u);
   unsigned hmax = 0u;
-  const bool adaptive = (mode & M_HIST) && !(kAblate & 32);
+  const bool adaptive = (mode & M_HIST) != 0;
   if (adaptive) {
     const unsigned* h = p.hist + view * kSlot;
     hb = reinterpret_cast<const uint4*>(h)[lane];
@@ -1477,7 +1264,6 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
   }
 
   *masked = 0;
-  if (!live) return 0;
 
   // ---- thresholds (while the loads above are in flight) ----
   int thr_w = 40, thr_c = 10;  // fixed: multi_point_cloud_process.py:36-38
@@ -1491,7 +1277,12 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
       p.stats[view].noise_floor = t.noise_floor;
       p.stats[view].dynamic_range = t.dynamic_range;
     }
+    // every wave of the view's workgroups reads the histogram: the last zeroes it
+    if (!p.rerun)
+      hist_release(p.hist + static_cast<int64_t>(view) * kSlot, kSlot, blockIdx.x * kWaves + (threadIdx.x >> 6),
+                   kWaves * gridDim.x, lane, t.white, t.contrast);
   }
+  if (!live) return 0;
 
   // ---- mask ----
   // vec: byte-SWAR in 16-bit lanes (even / odd pixels), two compares per 4
@@ -1572,7 +1363,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const unsigned c = (rc[s][e >> 1] >> (16 * (e & 1))) & 0x7fffu;
-        pf[e] = (kAblate & 128) ? make_float4(0.5f, 0.25f, 1.0f + 1e-3f * c, 0.0f) : p.planes32[c];
+        pf[e] = p.planes32[c];
       }
       ys = 0.0f;
       if (!nc) {
@@ -1598,10 +1389,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
     // table's largest sum|n_i| (sl_set_calib, rounded up): one compare per
     // pixel.  Masked pixels that fail it take the bounded test below.
     uint32_t todo = ok[s];
-    if (kAblate & 64) {
-      nib = todo;
-      todo = 0u;
-    } else if (vec && !nc) {
+    if (vec && !nc) {
       uint32_t fast = 0u;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -1660,11 +1448,8 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
 
 // k_count: one chunk per wave, grid (chunk groups of 4, views); the
 // workgroup's point total goes to block_sums for k_cloud's offsets.
-#ifndef SLGPU_COUNT_WAVES
-#define SLGPU_COUNT_WAVES 1
-#endif
 template <int VEC>
-__global__ __launch_bounds__(kThreads, SLGPU_COUNT_WAVES) void k_count(Params p) {
+__global__ __launch_bounds__(kThreads, 1) void k_count(Params p) {
   __shared__ int s_sum[kWaves];
   __shared__ int s_msum[kWaves];
   const int lane = threadIdx.x & 63;
@@ -1686,6 +1471,7 @@ __global__ __launch_bounds__(kThreads, SLGPU_COUNT_WAVES) void k_count(Params p)
     }
   }
   if (!(p.mode & M_CODES)) return;  // uniform: no barrier below
+  unsigned* const sup = super_produce(p);
   if (lane == 0) s_sum[wid] = total;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1694,82 +1480,28 @@ __global__ __launch_bounds__(kThreads, SLGPU_COUNT_WAVES) void k_count(Params p)
     for (int w = 0; w < kWaves; ++w) t += s_sum[w];
     const int64_t blk = static_cast<int64_t>(view) * gridDim.x + blockIdx.x;
     p.block_sums[blk] = t;
-    if (t) atomicAdd(p.super_sums + (blk >> p.sb_shift), static_cast<unsigned>(t));
+    if (t) atomicAdd(sup + (blk >> p.sb_shift), static_cast<unsigned>(t));
   }
 }
 
 // ================================================================= k_cloud ====
 // reconstruct_point_cloud's arithmetic (sl_system.py:584-653) for the points
-// k_count marked, one chunk per wave:
+// k_decode / k_count marked, one chunk per wave:
 //   0. the chunk's offset in the merged cloud: the super-block sums before its
-//      super-block + the chunk counts before it inside it (+ earlier launch
-//      groups);
+//      super-block + the block sums before it inside it (+ earlier launch
+//      groups), + the chunk counts of the workgroup's earlier waves;
 //   1. records + colour of the lane's 16 pixels (16-byte loads); the lane's
 //      point count and its exclusive prefix over the wave give every point its
 //      rank in the chunk (ascending pixel order, np.where, sl_system.py:601);
-//   2. each point's (pixel, column code) and BGR go to LDS at its rank -- the
-//      chunk's points, compacted;
-//   3. kPipe x 64 points per pass: lane j takes points j, j+64, ...; all their
+//   2. each point's (pixel, column code) goes to LDS at its rank -- the
+//      chunk's points, compacted -- and the chunk's texture bytes to LDS in
+//      pixel order;
+//   3. PIPE x 64 points per pass: lane j takes points j, j+64, ...; all their
 //      operand gathers (ray tables or Nc, plane) are issued before any point
-//      is computed, then the exact f64 arithmetic in the reference's operation
-//      order, then the stores at offset + rank (64 consecutive points per store
-//      instruction).
-#ifndef SLGPU_PIPE
-#define SLGPU_PIPE 4
-#endif
-constexpr int kPipe = SLGPU_PIPE;  // points per lane per pass in k_cloud
-#ifndef SLGPU_POSE_COARSE
-#define SLGPU_POSE_COARSE 1
-#endif
-constexpr bool kPoseCoarse = SLGPU_POSE_COARSE != 0;  // posed verified route: the coarse bound of M_k (A/B)
-#ifndef SLGPU_SMALL_PIPE
-#define SLGPU_SMALL_PIPE 4
-#endif
-constexpr int kSmallPipe = SLGPU_SMALL_PIPE;  // ... in launches of at most one chunk per SIMD (f32-fast)
-#ifndef SLGPU_STAGE_OUT
-#define SLGPU_STAGE_OUT 0
-#endif
-constexpr bool kStageOut = SLGPU_STAGE_OUT != 0;  // f32 points leave through an LDS stage
-#ifndef SLGPU_LDS_BGR
-#define SLGPU_LDS_BGR 2
-#endif
-// colour of a point: 1 = compacted with the entries in LDS, 2 = the chunk's
-// texture bytes in LDS in pixel order (3 B/px; 12 KB less LDS per workgroup
-// than 1), 0 = re-read from the texture in global memory
-constexpr int kBgrMode = SLGPU_LDS_BGR;
-constexpr bool kLdsBgr = kBgrMode == 1;
-constexpr bool kTexLds = kBgrMode == 2;
-constexpr int kBgrWords = kLdsBgr ? kChunk : kTexLds ? 3 * kChunk / 4 + 4 : 4;  // u32 per wave
-#ifndef SLGPU_TEX_COAL
-#define SLGPU_TEX_COAL 0
-#endif
-// k_cloud's texture loads as 1-KB rows of the chunk (each instruction whole
-// lines) instead of each lane's own 48 bytes (kTexLds only: the LDS copy is in
-// pixel order either way)
-constexpr bool kTexCoal = SLGPU_TEX_COAL != 0 && kTexLds;
-#ifndef SLGPU_COL_DWORD
-#define SLGPU_COL_DWORD 0
-#endif
-// (measurement build, SLGPU_COL_DWORD=1: k_cloud's colour bytes staged per
-// pass in LDS, 3 per point shifted to the pass's alignment in the output,
-// then stored 8 bytes per lane.  The byte / short stores of 3-byte colours
-// cost 4x the xyz stores per byte -- kbench, 8 4K views: 46 of 262 us for 157
-// MB of colours, 75 us for 629 MB of xyz -- but the stage costs more: k_cloud
-// 262 -> 328 us, c2 30.4 -> 46.3 us; bit-exact, 204 GPU tests)
-constexpr bool kColDword = SLGPU_COL_DWORD != 0;
-#ifndef SLGPU_COL_OVERLAP
-#define SLGPU_COL_OVERLAP 0
-#endif
-// (measurement build, SLGPU_COL_OVERLAP=1: k_cloud's colours as one 4-byte
-// store per point at its 3-byte slot, an unaligned buffer store whose 4th
-// byte is the next point's first colour byte -- taken from the next lane by
-// DPP, so both lanes writing that byte write the same value; the chunk's last
-// point writes its 3 bytes alone.  One store instruction per 64 points instead
-// of two, bit-exact (204 GPU tests), but slower: k_cloud 261.7 -> 264.0 us
-// for 8 4K views, c2 step 120.6 -> 122.3-123.6 us)
-constexpr bool kColOverlap = SLGPU_COL_OVERLAP != 0;
-constexpr int kColStage = 64 * 4 * 3 + 16;  // bytes per wave: up to 4 x 64 points + alignment
-
+//      is computed, then the arithmetic, then the stores at offset + rank (64
+//      consecutive points per store instruction).
+constexpr int kPipe = 4;  // points per lane per pass in the f32-fast k_cloud
+constexpr int kBgrWords = 3 * kChunk / 4 + 4;  // u32 per wave: the chunk's BGR bytes in pixel order (+ slack)
 
 // base + a 32-bit byte offset: the form global loads / stores take with an
 // SGPR base (wave-uniform pointer) and a 32-bit VGPR offset
@@ -1815,8 +1547,7 @@ struct ChunkIn {
   uint32_t ptbits;      // point bits of the 16 pixels (bit k: pixel 16 lane + k)
 };
 
-// Phase 1 of a chunk (global index gc): the lane's loads, issued by k_cloud
-// before its block-offset loads so that both round trips overlap.
+// Phase 1 of a chunk (global index gc): the lane's loads.
 template <int VEC>
 __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane, ChunkIn* in) {
   const bool vec = VEC > 0;
@@ -1827,26 +1558,7 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
   const int n_px = static_cast<int>(min<int64_t>(max<int64_t>(HW - px0, 0), kPx));
   const int64_t pxl = n_px > 0 ? px0 : 0;
   uint32_t* d = in->d;
-  if (p.rec_col) {  // the col map k_decode wrote, clipped (sl_system.py:626)
-    const int32_t* src = p.rec_col + view * HW + pxl;
-    const uint32_t cmax = static_cast<uint32_t>(p.Wp - 1);
-    uint32_t c[kPx];
-    if (vec) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint4 q = ld_side16(src + 4 * i);
-        c[4 * i] = q.x;
-        c[4 * i + 1] = q.y;
-        c[4 * i + 2] = q.z;
-        c[4 * i + 3] = q.w;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kPx; ++k) c[k] = k < n_px ? static_cast<uint32_t>(src[k]) : 0u;
-    }
-#pragma unroll
-    for (int i = 0; i < kPx / 2; ++i) d[i] = min(c[2 * i], cmax) | (min(c[2 * i + 1], cmax) << 16);
-  } else if (vec && p.rec12) {  // 12-bit records (k_decode): 8 codes per 3 words
+  if (vec && p.rec12) {  // 12-bit records (k_decode M_DECIDE): 8 codes per 3 words
     in->ptbits = 0u;
     uint32_t w[6];
     if (p.rec_blk) {  // the chunk's slot: words 0-3 at 16 lane, 4-5 at 1024 + 8 lane
@@ -1901,32 +1613,7 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
   uint4* tq = in->tq;
   if (p.tex != nullptr) {
     const uint8_t* t = p.tex + view * p.tex_vs + 3 * pxl;
-    if (vec && kTexCoal) {
-      // the chunk's 3 KB of texture as three 1-KB rows (lane: 16 B at 16 lane
-      // + 1024 i), so that each load instruction covers whole lines; k_cloud
-      // stores them to LDS at the same offsets (pixel order, kTexLds).  Rows
-      // past the view's texture (its last, partial chunk) re-read its last 16
-      // bytes: those pixels make no points.
-      const int64_t tv = 3 * HW;
-      const uint8_t* tb = p.tex + view * p.tex_vs;
-      const int64_t c0 = 3 * static_cast<int64_t>(civ) * kChunk + 16 * lane;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const uint8_t* a = tb + min<int64_t>(c0 + 1024 * i, tv - 16);
-        if (SLGPU_NT_TEX) {
-          const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(a));
-          tq[i] = make_uint4(q.x, q.y, q.z, q.w);
-        } else {
-          tq[i] = ld_side16(a);
-        }
-      }
-    } else if (vec && SLGPU_NT_TEX) {  // (A/B) non-temporal texture loads (read once)
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const v4u q = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(t + 16 * i));
-        tq[i] = make_uint4(q.x, q.y, q.z, q.w);
-      }
-    } else if (vec) {
+    if (vec) {
       tq[0] = ld_side16(t);
       tq[1] = ld_side16(t + 16);
       tq[2] = ld_side16(t + 32);
@@ -1947,97 +1634,13 @@ __device__ __forceinline__ void cloud_load(const Params& p, int64_t gc, int lane
   }
 }
 
-// Phases 2-3 of a chunk (global index gc, output offset base), by one wave,
-// from the lane's loads.
-template <int MODE, int VEC, int PIPE>
-__device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
-                                             int total, const uint32_t* s_ent, const uint32_t* s_bgr,
-                                             float* s_sxyz, uint8_t* s_scol, bool col_stage);
-
-template <int MODE, int VEC, int PIPE>
-__device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane, const ChunkIn& in,
-                                            uint32_t* s_ent, uint32_t* s_bgr, float* s_sxyz, uint8_t* s_scol, bool col_stage = false) {
-  const int view = static_cast<int>(gc / p.cpv);
-  const int civ = static_cast<int>(gc - static_cast<int64_t>(view) * p.cpv);
-  const int64_t cpx = static_cast<int64_t>(civ) * kChunk;  // chunk's first pixel
-  const int mode = MODE >= 0 ? MODE : p.mode;
-  const bool has_tex = (mode & M_TEX) != 0;
-  // 16-byte path (W % 16 == 0, W >= 64): a lane's 16 pixels share one image
-  // row, at most 17 rows below the chunk's first; the row offset rides in
-  // the entry (bits 25..29) so that cloud_points needs no division
-  uint32_t drow = 0u;
-  if (VEC > 0) {
-    const int px = static_cast<int>(cpx) + lane * kPx;  // < HW < 2^31
-    drow = static_cast<uint32_t>(px / p.W - static_cast<int>(cpx) / p.W) << 25;
-  }
-  const uint32_t* d = in.d;
-  const uint4* tq = in.tq;
-  const uint32_t ptbits = in.ptbits;
-  __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads come first
-  const int n_l = __popc(ptbits);
-  const int incl = wave_incl_scan(n_l, lane);
-  const int total = __shfl(incl, 63, 64);
-  if (lane == 0 && civ == 0) p.view_offsets[view] = base;
-  // offsets past the caller's capacity can only come from scratch out of
-  // phase with its launches (e.g. a captured graph replayed when its launch
-  // count is not a multiple of the scratch rotations, slgpu.h): write nothing
-  // (the call's total then exceeds the capacity, which the host reports)
-  if (base < 0 || base + total > p.out_cap) return;
-  if (kAblate & 8) {  // measurement only: stop after the loads and the rank scan
-    if (total == -1) p.bgr[0] = static_cast<uint8_t>(d[0] ^ tq[0].x ^ tq[1].y ^ tq[2].z);
-    return;
-  }
-
-  // ---- 2. compacted entries in LDS (and the chunk's colours, kTexLds) ----
-  if (kTexLds) {
-    uint4* t4 = reinterpret_cast<uint4*>(s_bgr);
-    if (has_tex && kTexCoal && VEC > 0) {  // (cloud_load's 1-KB rows)
-      t4[lane] = tq[0];
-      t4[64 + lane] = tq[1];
-      t4[128 + lane] = tq[2];
-    } else if (has_tex) {
-      t4[3 * lane] = tq[0];
-      t4[3 * lane + 1] = tq[1];
-      t4[3 * lane + 2] = tq[2];
-    } else {
-      t4[lane] = tq[0];  // gray bytes, one per pixel
-    }
-  }
-  {
-    int idx = incl - n_l;
-#pragma unroll
-    for (int k = 0; k < kPx; ++k) {
-      const uint32_t code = (d[k >> 1] >> (16 * (k & 1))) & 0x7fffu;
-      uint32_t bgr;
-      if (has_tex) {
-        const int b = 3 * k;
-        bgr = byte_of(tq[b >> 4], b & 15) | (byte_of(tq[(b + 1) >> 4], (b + 1) & 15) << 8) |
-              (byte_of(tq[(b + 2) >> 4], (b + 2) & 15) << 16);
-      } else {
-        bgr = byte_of(tq[0], k) * 0x010101u;
-      }
-      if ((ptbits >> k) & 1u) {
-        s_ent[idx] = static_cast<uint32_t>(lane * kPx + k) | (code << 10) | drow;
-        if (kLdsBgr) s_bgr[idx] = bgr;
-        (void)bgr;
-      }
-      idx += (ptbits >> k) & 1u;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  if (kAblate & 16) return;  // measurement only: stop after the LDS compaction
-
-  cloud_points<MODE, VEC, PIPE>(p, view, cpx, base, lane, total, s_ent, s_bgr, s_sxyz, s_scol, col_stage);
-}
-
 // Phase 3 of a chunk: its `total` compacted points (s_ent: pixel | code << 10
-// | row offset << 25 on the 16-byte path, s_bgr: colour) -> xyz + BGR at
-// offset base + rank, kPipe x 64 per pass.
+// | row offset << 25 on the 16-byte path, s_bgr: the chunk's colours in pixel
+// order) -> xyz + BGR at offset base + rank, PIPE x 64 per pass.
 template <int MODE, int VEC, int PIPE>
 __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t cpx, long long base, int lane,
-                                             int total, const uint32_t* s_ent, const uint32_t* s_bgr,
-                                             float* s_sxyz, uint8_t* s_scol, bool col_stage) {
-  constexpr int kPipe = PIPE;  // points per lane per pass
+                                             int total, const uint32_t* s_ent, const uint32_t* s_bgr) {
+  constexpr int kP = PIPE;  // points per lane per pass
   const int mode = MODE >= 0 ? MODE : p.mode;
   const int64_t HW = p.HW;
   const bool has_tex = (mode & M_TEX) != 0;
@@ -2072,29 +1675,22 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
     }
   }
   const bool f64out = (mode & M_XYZ64) != 0;
-  constexpr int dbg = kAblate;
-  auto point_bgr = [&](int j, int local) -> uint32_t {
-    if (kLdsBgr) return s_bgr[j];
-    if (kTexLds) {
-      if (has_tex) {  // bytes 3 local .. 3 local + 2 of the chunk's BGR
-        const int b = 3 * local;
-        const uint32_t w0 = s_bgr[b >> 2], w1 = s_bgr[(b >> 2) + 1];
-        return __builtin_amdgcn_alignbyte(w1, w0, static_cast<unsigned>(b & 3)) & 0xffffffu;
-      }
-      return ((s_bgr[local >> 2] >> (8 * (local & 3))) & 0xffu) * 0x010101u;
+  auto point_bgr = [&](int local) -> uint32_t {
+    if (has_tex) {  // bytes 3 local .. 3 local + 2 of the chunk's BGR
+      const int b = 3 * local;
+      const uint32_t w0 = s_bgr[b >> 2], w1 = s_bgr[(b >> 2) + 1];
+      return __builtin_amdgcn_alignbyte(w1, w0, static_cast<unsigned>(b & 3)) & 0xffffffu;
     }
-    if (has_tex) {
-      const uint8_t* t = p.tex + view * p.tex_vs + 3 * (cpx + local);
-      return t[0] | (static_cast<uint32_t>(t[1]) << 8) | (static_cast<uint32_t>(t[2]) << 16);
-    }
-    return static_cast<uint32_t>(p.stack[view * p.stack_vs + cpx + local]) * 0x010101u;
+    return ((s_bgr[local >> 2] >> (8 * (local & 3))) & 0xffu) * 0x010101u;
   };
   float* const wx = static_cast<float*>(p.xyz) + 3 * base;  // the chunk's first point (wave-uniform)
   uint8_t* const wc = p.bgr + 3 * base;
-  // (kColOverlap) the chunk's colour bytes [3 base, 3 (base + total)) as a
-  // buffer: SGPR base, 32-bit lane offsets, nothing written past its end
-  const __amdgpu_buffer_rsrc_t rs_col = __builtin_amdgcn_make_buffer_rsrc(wc, 0, 3 * total, 0x00020000);
-  for (int j0 = 0; j0 < total; j0 += 64 * kPipe) {
+  // (The colours leave as a short and a byte store per point.  Round 5
+  // measured the register-only form -- every 64 points' 192 colour bytes
+  // assembled by lane permutes into 48 aligned dwords, one store instruction
+  // -- and it was slower: c2 124.1-125.4 -> 127.3-127.4 us per step, c5 3.554
+  // -> 3.671 ms, same box (profiles/r05_ab/colour_pack_lines.jsonl).)
+  for (int j0 = 0; j0 < total; j0 += 64 * kP) {
     if (mode & M_FAST32) {
       // SL_XYZ_F32_FAST (Oc = 0, pinhole rays, no pose; host-checked): the
       // same formula in f32 -- rsq-normalised ray, f32 plane, rcp -- for
@@ -2102,29 +1698,22 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       // kFastKappa; the rest take the exact f64 route below.  Per-coordinate
       // relative error vs the reference's f64 <= (11 + 10 kappa) 2^-24
       // ("f32-fast").
-      float fx[kPipe], fy[kPipe];
-      float4 fp[kPipe];
-      uint32_t bgr[kPipe];
+      float fx[kP], fy[kP];
+      float4 fp[kP];
+      uint32_t bgr[kP];
 #pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
+      for (int i = 0; i < kP; ++i) {
         const int j = min(j0 + 64 * i + lane, total - 1);
         const uint32_t e = s_ent[j];
-        const int local = static_cast<int>(e & 1023u);
-        bgr[i] = point_bgr(j, local);
+        bgr[i] = point_bgr(static_cast<int>(e & 1023u));
         int uu, vv;
         chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
-        if (kAblate & 512) {  // measurement only: no table gathers
-          fx[i] = 0.001f * static_cast<float>(uu);
-          fy[i] = 0.001f * static_cast<float>(vv);
-          fp[i] = make_float4(0.1f, 0.2f, 0.9f, -500.0f - static_cast<float>(ent_code(e)));
-          continue;
-        }
         fx[i] = *at_bytes(p.xn32, 4u * static_cast<unsigned>(uu));
         fy[i] = *at_bytes(p.yn32, 4u * static_cast<unsigned>(vv));
         fp[i] = p.planes32[ent_code(e)];
       }
 #pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
+      for (int i = 0; i < kP; ++i) {
         const int j = j0 + 64 * i + lane;
         const float x = fx[i], y = fy[i];
         const float inv = __builtin_amdgcn_rsqf((x * x + y * y) + 1.0f);
@@ -2151,9 +1740,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           Y = static_cast<float>(p.o1 + d1 * td);
           Z = static_cast<float>(p.o2 + d2 * td);
         }
-        if (kAblate & 256) {  // measurement only: no point stores (results kept live)
-          if (X == -1234.5f && Y == Z) p.bgr[0] = static_cast<uint8_t>(bgr[i]);
-        } else if (j < total) {
+        if (j < total) {
           float* xyz = at_bytes(wx, 12u * static_cast<unsigned>(j));
           xyz[0] = X;
           xyz[1] = Y;
@@ -2166,23 +1753,15 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       }
       continue;
     }
-    double ra[kPipe], rb[kPipe], rcz[kPipe];  // pinhole: x, y, -; Nc: r0, r1, r2
-    double4 pl[kPipe];
-    uint32_t bgr[kPipe];
+    double ra[kP], rb[kP], rcz[kP];  // pinhole: x, y, -; Nc: r0, r1, r2
+    double4 pl[kP];
+    uint32_t bgr[kP];
 #pragma unroll
-    for (int i = 0; i < kPipe; ++i) {
+    for (int i = 0; i < kP; ++i) {
       const int j = min(j0 + 64 * i + lane, total - 1);  // past the end: repeat the last point
       const uint32_t e = s_ent[j];
       const int local = static_cast<int>(e & 1023u);
-      bgr[i] = point_bgr(j, local);
-      const unsigned c = ent_code(e);
-      if (dbg & 4) {
-        ra[i] = 0.25 + local;
-        rb[i] = 0.5;
-        rcz[i] = 1.0;
-        pl[i] = make_double4(0.1, 0.2, 0.9, -500.0 - c);
-        continue;
-      }
+      bgr[i] = point_bgr(local);
       if (mode & M_NC) {
         const int64_t q = cpx + local;
         ra[i] = p.nc_rays[q];
@@ -2197,7 +1776,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           // fallback re-reads the tables)
           ra[i] = (static_cast<double>(uu) - p.cx) * p.rfx;
           rb[i] = (static_cast<double>(vv) - p.cy) * p.rfy;
-        } else if (kXyCalc && p.xy_calc) {  // (uniform) the table values, computed: no 16 B of gathers per point
+        } else if (p.xy_calc) {  // (uniform) the table values, computed: no 16 B of gathers per point
           ra[i] = xy_of(uu, p.cx, p.fx);  // (gathering x or y instead: +0.8 / +1.1 us at c2)
           rb[i] = xy_of(vv, p.cy, p.fy);
         } else {
@@ -2205,18 +1784,10 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           rb[i] = p.yn[vv];
         }
       }
-      pl[i] = p.planes[(dbg & 1024) ? (c & 31u) : c];  // (1024: measurement only, a 1-KB plane table)
+      pl[i] = p.planes[ent_code(e)];
     }
-    double X[kPipe], Y[kPipe], Z[kPipe];
+    double X[kP], Y[kP], Z[kP];
     uint32_t slow = 0u;
-    if (dbg & 4096) {  // measurement only: no point arithmetic at all (operands stored as the point)
-#pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
-        X[i] = ra[i];
-        Y[i] = rb[i];
-        Z[i] = pl[i].w + pl[i].x;
-      }
-    } else {
     if (mode & M_VERIFY) {
       // SL_XYZ_F32 output is float32(P_ref), P_ref the reference's f64 value
       // (sl_system.py:614-648 with Oc = 0, pinhole rays, no pose).  With
@@ -2249,7 +1820,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         return static_cast<unsigned>(!(fabs(v) >= 0x1p-80)) | static_cast<unsigned>(!(fabs(v) < 0x1p80));
       };
 #pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
+      for (int i = 0; i < kP; ++i) {
         const double x = ra[i], y = rb[i];
         // n . v and sum |n_i v_i| by fused multiply-adds: two roundings each,
         // fewer than the products-then-sums the bound below allows for
@@ -2280,21 +1851,14 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           const double X2 = fma(pm[0], x0, fma(pm[1], x1, fma(pm[2], x2, pm[3])));
           const double Y2 = fma(pm[4], x0, fma(pm[5], x1, fma(pm[6], x2, pm[7])));
           const double Z2 = fma(pm[8], x0, fma(pm[9], x1, fma(pm[10], x2, pm[11])));
-          double M0, M1, M2;  // 2^-44 M_k (the scale folded into pb / pt: exact)
-          if (kPoseCoarse) {
-            // M_k <= R_k max_j |P_j| + |m_k3| (R_k = sum_j |m_kj|, per view):
-            // a wider interval, so as safe, at 4 operations instead of 18
-            // (the slack of 2^-44 against the 2^-45.2 the bound needs covers
-            // these few roundings)
-            const double pmax = fmax(fmax(fabs(x0), fabs(x1)), fabs(x2));
-            M0 = fma(pb[0], pmax, pt[0]);
-            M1 = fma(pb[1], pmax, pt[1]);
-            M2 = fma(pb[2], pmax, pt[2]);
-          } else {
-            M0 = 0x1p-44 * (((fabs(pm[0] * x0) + fabs(pm[1] * x1)) + fabs(pm[2] * x2)) + fabs(pm[3]));
-            M1 = 0x1p-44 * (((fabs(pm[4] * x0) + fabs(pm[5] * x1)) + fabs(pm[6] * x2)) + fabs(pm[7]));
-            M2 = 0x1p-44 * (((fabs(pm[8] * x0) + fabs(pm[9] * x1)) + fabs(pm[10] * x2)) + fabs(pm[11]));
-          }
+          // 2^-44 M_k <= 2^-44 (R_k max_j |P_j| + |m_k3|) (R_k = sum_j |m_kj|,
+          // per view, the scale folded into pb / pt: exact): a wider interval,
+          // so as safe, at 4 operations instead of 18 (the slack of 2^-44
+          // against the 2^-45.2 the bound needs covers these few roundings)
+          const double pmax = fmax(fmax(fabs(x0), fabs(x1)), fabs(x2));
+          const double M0 = fma(pb[0], pmax, pt[0]);
+          const double M1 = fma(pb[1], pmax, pt[1]);
+          const double M2 = fma(pb[2], pmax, pt[2]);
           bad |= unsettled(X2, M0) | unsettled(Y2, M1) | unsettled(Z2, M2);
           X[i] = X2;
           Y[i] = Y2;
@@ -2305,7 +1869,7 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         slow |= (bad & 1u) << i;
       }
     }
-    // The kPipe points' chains (sqrt, shared reciprocal, divisions) carry no
+    // The kP points' chains (sqrt, shared reciprocal, divisions) carry no
     // branch, so the compiler interleaves them: a point whose operands leave
     // the range where the shortened sequences are bit-identical to the
     // operators (div_safe) only sets its bit in `slow`, and is recomputed
@@ -2318,72 +1882,67 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
     uint32_t fallback = (mode & M_VERIFY) ? slow : 0u;  // points for the operators' own sequences
     slow = 0u;
     if (!(mode & M_VERIFY)) {
-    // stage by stage over the kPipe points (the source order the scheduler
-    // keeps): independent instructions of different points sit side by side
-    double r0[kPipe], r1[kPipe], r2[kPipe];
-    if (mode & M_NC) {
+      // stage by stage over the kP points (the source order the scheduler
+      // keeps): independent instructions of different points sit side by side
+      double r0[kP], r1[kP], r2[kP];
+      if (mode & M_NC) {
 #pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
-        r0[i] = ra[i];
-        r1[i] = rb[i];
-        r2[i] = rcz[i];
+        for (int i = 0; i < kP; ++i) {
+          r0[i] = ra[i];
+          r1[i] = rb[i];
+          r2[i] = rcz[i];
+        }
+      } else {
+        double nrm[kP], rn[kP];
+#pragma unroll
+        for (int i = 0; i < kP; ++i) {
+          const double x = ra[i], y = rb[i];
+          nrm[i] = sqrt_nr((x * x + y * y) + 1.0);  // s2 in [1, 2^601] when div_safe(x), div_safe(y)
+          if (!(p.xy_safe || (div_safe(x) && div_safe(y)))) slow |= 1u << i;
+        }
+        // the three divisions by nrm share one reciprocal (div_rn: the
+        // compiler's own f64 division sequence, bit for bit, where it would
+        // not rescale)
+#pragma unroll
+        for (int i = 0; i < kP; ++i) rn[i] = recip_nr(nrm[i]);
+#pragma unroll
+        for (int i = 0; i < kP; ++i) {
+          r0[i] = div_rn(ra[i], nrm[i], rn[i]);
+          r1[i] = div_rn(rb[i], nrm[i], rn[i]);
+          r2[i] = div_rn(1.0, nrm[i], rn[i]);
+        }
       }
-    } else {
-      double nrm[kPipe], rn[kPipe];
+      double den[kP], t[kP];
 #pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
-        const double x = ra[i], y = rb[i];
-        nrm[i] = sqrt_nr((x * x + y * y) + 1.0);  // s2 in [1, 2^601] when div_safe(x), div_safe(y)
-        if (!(kDivShare && (p.xy_safe || (div_safe(x) && div_safe(y))))) slow |= 1u << i;
+      for (int i = 0; i < kP; ++i) den[i] = (pl[i].x * r0[i] + pl[i].y * r1[i]) + pl[i].z * r2[i];
+#pragma unroll
+      for (int i = 0; i < kP; ++i) {
+        t[i] = div_rn(-pl[i].w, den[i], recip_nr(den[i]));
+        if (!(div_safe(pl[i].w) && div_safe(den[i]))) slow |= 1u << i;
       }
-      // the three divisions by nrm share one reciprocal (div_rn: the
-      // compiler's own f64 division sequence, bit for bit, where it would
-      // not rescale)
 #pragma unroll
-      for (int i = 0; i < kPipe; ++i) rn[i] = recip_nr(nrm[i]);
-#pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
-        r0[i] = div_rn(ra[i], nrm[i], rn[i]);
-        r1[i] = div_rn(rb[i], nrm[i], rn[i]);
-        r2[i] = div_rn(1.0, nrm[i], rn[i]);
+      for (int i = 0; i < kP; ++i) {
+        X[i] = p.o0 + r0[i] * t[i];
+        Y[i] = p.o1 + r1[i] * t[i];
+        Z[i] = p.o2 + r2[i] * t[i];
       }
-    }
-    double den[kPipe], t[kPipe];
-#pragma unroll
-    for (int i = 0; i < kPipe; ++i) den[i] = (pl[i].x * r0[i] + pl[i].y * r1[i]) + pl[i].z * r2[i];
-#pragma unroll
-    for (int i = 0; i < kPipe; ++i) {
-      t[i] = div_rn(-pl[i].w, den[i], recip_nr(den[i]));
-      if (!(kDivShare && div_safe(pl[i].w) && div_safe(den[i]))) slow |= 1u << i;
-    }
-#pragma unroll
-    for (int i = 0; i < kPipe; ++i) {
-      X[i] = p.o0 + r0[i] * t[i];
-      Y[i] = p.o1 + r1[i] * t[i];
-      Z[i] = p.o2 + r2[i] * t[i];
-      if (dbg & 1) {
-        X[i] = ra[i];
-        Y[i] = rb[i];
-        Z[i] = pl[i].w;
-      }
-    }
-    fallback = slow;
+      fallback = slow;
     }  // !M_VERIFY
     if (fallback) {  // rare: the operators' own sequences (rescaling, +-0, inf / NaN; unsettled M_VERIFY points)
 #pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
+      for (int i = 0; i < kP; ++i) {
         if (!((fallback >> i) & 1u)) continue;
         // the point's operands again (M_VERIFY: re-read, so that nothing of
         // the verified route stays live across this block)
         double xa = ra[i], xb = rb[i], xc = rcz[i];
         double4 pp = pl[i];
-        if ((mode & M_VERIFY) && !(dbg & 4)) {
+        if (mode & M_VERIFY) {
           const uint32_t e = s_ent[min(j0 + 64 * i + lane, total - 1)];
           int uu, vv;
           chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
           xa = p.xn[uu];
           xb = p.yn[vv];
-          pp = p.planes[(dbg & 1024) ? (ent_code(e) & 31u) : ent_code(e)];
+          pp = p.planes[ent_code(e)];
         }
         double r0, r1, r2;
         if (mode & M_NC) {
@@ -2412,10 +1971,9 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         }
       }
     }
-    }  // dbg & 4096
     if (pose && !(mode & M_VERIFY)) {
 #pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
+      for (int i = 0; i < kP; ++i) {
         const double X2 = ((pm[0] * X[i] + pm[1] * Y[i]) + pm[2] * Z[i]) + pm[3];
         const double Y2 = ((pm[4] * X[i] + pm[5] * Y[i]) + pm[6] * Z[i]) + pm[7];
         const double Z2 = ((pm[8] * X[i] + pm[9] * Y[i]) + pm[10] * Z[i]) + pm[11];
@@ -2424,42 +1982,8 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         Z[i] = Z2;
       }
     }
-    if (dbg & 2) continue;
-    if (kStageOut && !f64out) {
-      // 64 points at a time through an LDS stage: their 192 xyz words and 192
-      // colour bytes leave as lane-consecutive dword / byte stores
 #pragma unroll
-      for (int i = 0; i < kPipe; ++i) {
-        const int j = j0 + 64 * i + lane;
-        const int n = min(64, total - (j0 + 64 * i));
-        if (n <= 0) break;
-        s_sxyz[3 * lane] = static_cast<float>(X[i]);
-        s_sxyz[3 * lane + 1] = static_cast<float>(Y[i]);
-        s_sxyz[3 * lane + 2] = static_cast<float>(Z[i]);
-        s_scol[3 * lane] = static_cast<uint8_t>(bgr[i]);
-        s_scol[3 * lane + 1] = static_cast<uint8_t>(bgr[i] >> 8);
-        s_scol[3 * lane + 2] = static_cast<uint8_t>(bgr[i] >> 16);
-        __builtin_amdgcn_wave_barrier();
-        const long long o = base + (j - lane);
-        float* xyz = static_cast<float*>(p.xyz) + 3 * o;
-        uint8_t* cc = p.bgr + 3 * o;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          if (64 * k + lane < 3 * n) {
-            xyz[64 * k + lane] = s_sxyz[64 * k + lane];
-            cc[64 * k + lane] = s_scol[64 * k + lane];
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-      continue;
-    }
-    // (col_stage: the colours through the wave's LDS stage, shifted by the
-    // pass's first output byte modulo 8, then 8 bytes per lane)
-    const bool cst = col_stage && !(kAblate & 16384);
-    const int csh = static_cast<int>((3 * (base + j0)) & 7);
-#pragma unroll
-    for (int i = 0; i < kPipe; ++i) {
+    for (int i = 0; i < kP; ++i) {
       const int j = j0 + 64 * i + lane;
       if (j < total) {
         const unsigned o = static_cast<unsigned>(j);  // offset from the chunk's first point
@@ -2468,37 +1992,11 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           xyz[0] = X[i];
           xyz[1] = Y[i];
           xyz[2] = Z[i];
-        } else if (kAblate & 32768) {  // measurement only: no xyz stores (kept live)
-          if (X[i] == -1234.5 && Y[i] == Z[i]) p.bgr[0] = 1;
         } else {
           float* xyz = at_bytes(wx, 12u * o);
           xyz[0] = static_cast<float>(X[i]);
           xyz[1] = static_cast<float>(Y[i]);
           xyz[2] = static_cast<float>(Z[i]);
-        }
-        if (kAblate & 16384) {  // measurement only: no colour stores (kept live)
-          if (bgr[i] == 0x12345678u) p.bgr[1] = 1;
-          continue;
-        }
-        if (kColOverlap && !cst) {
-          // the next point's colour: lane + 1 of this slot, or lane 0 of the next
-          const uint32_t nx = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(bgr[i]), 0x130, 0xf, 0xf, false));
-          const uint32_t nn = (i + 1 < kPipe) ? static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(bgr[i + 1 < kPipe ? i + 1 : i]))) : 0u;
-          const uint32_t next = lane == 63 ? nn : nx;
-          if (j + 1 < total && (lane < 63 || i + 1 < kPipe)) {
-            __builtin_amdgcn_raw_buffer_store_b32((bgr[i] & 0xffffffu) | (next << 24), rs_col, 3 * static_cast<int>(o), 0, 0);
-          } else {  // the chunk's last point (or a pass's last lane with no next slot): 3 bytes
-            __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(bgr[i]), rs_col, 3 * static_cast<int>(o), 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b8(static_cast<unsigned char>(bgr[i] >> 16), rs_col, 3 * static_cast<int>(o) + 2, 0, 0);
-          }
-          continue;
-        }
-        if (cst) {
-          uint8_t* sc = s_scol + csh + 3 * (64 * i + lane);
-          sc[0] = static_cast<uint8_t>(bgr[i]);
-          sc[1] = static_cast<uint8_t>(bgr[i] >> 8);
-          sc[2] = static_cast<uint8_t>(bgr[i] >> 16);
-          continue;
         }
         uint8_t* cc = at_bytes(wc, 3u * o);
         cc[0] = static_cast<uint8_t>(bgr[i]);
@@ -2506,59 +2004,84 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         cc[2] = static_cast<uint8_t>(bgr[i] >> 16);
       }
     }
-    if (cst) {
-      // the pass's colour bytes [A, A + 3n), A = 3 (base + j0), from the stage
-      // (byte k of the stage = output byte A - csh + k) to the 8-byte aligned
-      // words that cover them: whole words by one 8-byte store; the first and
-      // last (shared with the neighbouring passes / chunks) byte by byte
-      __builtin_amdgcn_wave_barrier();
-      const int nbytes = csh + 3 * min(64 * kPipe, total - j0);
-      // a buffer descriptor of the pass's 8-byte aligned output (SGPRs, per
-      // pass) + the lane's 32-bit offset: no 64-bit VGPR address stays live
-      // across passes (one did, and spilled)
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          p.bgr + (3 * (base + j0) - csh), 0, nbytes, 0x00020000);
-#pragma unroll
-      for (int q0 = 0; q0 < (3 * 64 * kPipe + 7 + 7) / 8; q0 += 64) {
-        const int b0 = 8 * (q0 + lane);
-        if (b0 < nbytes) {
-          if (b0 >= csh && b0 + 8 <= nbytes) {
-            const uint2 w = *reinterpret_cast<const uint2*>(s_scol + b0);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, w), rs, b0, 0, 0);
-          } else {
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if (b0 + k >= csh && b0 + k < nbytes) __builtin_amdgcn_raw_buffer_store_b8(s_scol[b0 + k], rs, b0 + k, 0, 0);
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();  // (the next pass rewrites the stage)
-    }
   }
 }
 
-// k_cloud: one chunk per wave, grid as k_count.  The workgroup's output
-// offset is the sum of k_count's block sums before it (+ the earlier launch
-// groups of the call); each wave adds the counts of the chunks before it in
-// the workgroup.
+// Phases 2-3 of a chunk (global index gc, output offset base), by one wave,
+// from the lane's loads.
+template <int MODE, int VEC, int PIPE>
+__device__ __forceinline__ void cloud_chunk(const Params& p, int64_t gc, long long base, int lane, const ChunkIn& in,
+                                            uint32_t* s_ent, uint32_t* s_bgr) {
+  const int view = static_cast<int>(gc / p.cpv);
+  const int civ = static_cast<int>(gc - static_cast<int64_t>(view) * p.cpv);
+  const int64_t cpx = static_cast<int64_t>(civ) * kChunk;  // chunk's first pixel
+  const int mode = MODE >= 0 ? MODE : p.mode;
+  const bool has_tex = (mode & M_TEX) != 0;
+  // 16-byte path (W % 16 == 0, W >= 64): a lane's 16 pixels share one image
+  // row, at most 17 rows below the chunk's first; the row offset rides in
+  // the entry (bits 25..29) so that cloud_points needs no division
+  uint32_t drow = 0u;
+  if (VEC > 0) {
+    const int px = static_cast<int>(cpx) + lane * kPx;  // < HW < 2^31
+    drow = static_cast<uint32_t>(px / p.W - static_cast<int>(cpx) / p.W) << 25;
+  }
+  const uint32_t* d = in.d;
+  const uint4* tq = in.tq;
+  const uint32_t ptbits = in.ptbits;
+  __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads come first
+  const int n_l = __popc(ptbits);
+  const int incl = wave_incl_scan(n_l, lane);
+  const int total = __builtin_amdgcn_readlane(incl, 63);
+  if (lane == 0 && civ == 0) p.view_offsets[view] = base;
+  // offsets past the caller's capacity (a caller's buffer smaller than its
+  // declared capacity cannot be detected; this guards the declared one):
+  // write nothing (the call's total then exceeds the capacity, which the host
+  // reports)
+  if (base < 0 || base + total > p.out_cap) return;
+
+  // ---- 2. compacted entries in LDS, the chunk's colours in pixel order ----
+  {
+    uint4* t4 = reinterpret_cast<uint4*>(s_bgr);
+    if (has_tex) {
+      t4[3 * lane] = tq[0];
+      t4[3 * lane + 1] = tq[1];
+      t4[3 * lane + 2] = tq[2];
+    } else {
+      t4[lane] = tq[0];  // gray bytes, one per pixel
+    }
+  }
+  {
+    int idx = incl - n_l;
+#pragma unroll
+    for (int k = 0; k < kPx; ++k) {
+      const uint32_t code = (d[k >> 1] >> (16 * (k & 1))) & 0x7fffu;
+      if ((ptbits >> k) & 1u) s_ent[idx] = static_cast<uint32_t>(lane * kPx + k) | (code << 10) | drow;
+      idx += (ptbits >> k) & 1u;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  cloud_points<MODE, VEC, PIPE>(p, view, cpx, base, lane, total, s_ent, s_bgr);
+}
+
+// k_cloud: one chunk per wave, grid (triangulating workgroups per view +
+// pre-stats workgroups, views).  The workgroup's output offset is the sum of
+// the block sums before it (+ the earlier launch groups of the call); each
+// wave adds the counts of the chunks before it in the workgroup.
 constexpr int kPrefixBatch = 4;
-#ifndef SLGPU_CLOUD_HOIST
-#define SLGPU_CLOUD_HOIST 0
-#endif
-constexpr bool kCloudHoist = SLGPU_CLOUD_HOIST != 0;  // chunk loads issued before the block-offset loads
 
 // Points of the blocks before block b of the launch group (one workgroup;
 // holds a workgroup barrier): the super-block sums before b's super-block,
 // then the block sums before b inside it (both <= ~sqrt(blocks) entries; all
-// loads of a batch in flight together).
-__device__ __forceinline__ long long block_offset(const Params& p, int64_t b, int tid, int lane, int wid,
-                                                  long long* s_wred) {
+// loads of a batch in flight together).  Every wave's loads have returned
+// when it returns (their sums crossed the barrier).
+__device__ __forceinline__ long long block_offset(const Params& p, const unsigned* sup, int64_t b, int tid, int lane,
+                                                  int wid, long long* s_wred) {
   long long acc = 0;
   const int64_t sb = b >> p.sb_shift;
   for (int64_t t0 = 0; t0 < sb; t0 += kPrefixBatch * kThreads) {
     unsigned v[kPrefixBatch];
 #pragma unroll
-    for (int i = 0; i < kPrefixBatch; ++i) v[i] = p.super_sums[min<int64_t>(t0 + i * kThreads + tid, sb - 1)];
+    for (int i = 0; i < kPrefixBatch; ++i) v[i] = sup[min<int64_t>(t0 + i * kThreads + tid, sb - 1)];
 #pragma unroll
     for (int i = 0; i < kPrefixBatch; ++i) acc += (t0 + i * kThreads + tid < sb) ? v[i] : 0u;
   }
@@ -2578,189 +2101,41 @@ __device__ __forceinline__ long long block_offset(const Params& p, int64_t b, in
   return t;
 }
 
-// PIPE: points per lane per pass (kPipe; launches of at most one chunk per
-// SIMD take all of a chunk's points in one pass: one gather round trip)
-#ifndef SLGPU_CLOUD_WAVES
-#define SLGPU_CLOUD_WAVES 5
-#endif
-#ifndef SLGPU_EXACT_PIPE
-#define SLGPU_EXACT_PIPE 2
-#endif
-constexpr int kExactPipe = SLGPU_EXACT_PIPE;  // points per lane per pass of the exact (f64) k_cloud<M_TEX>
-#ifndef SLGPU_VERIFY_PIPE
-#define SLGPU_VERIFY_PIPE 2
-#endif
-constexpr int kVerifyPipe = SLGPU_VERIFY_PIPE;  // ... of the verified-route k_cloud<M_VERIFY | M_TEX>
+// PIPE: points per lane per pass (the f64 chains: 2; f32-fast: kPipe)
+constexpr int kExactPipe = 2;   // points per lane per pass of the exact (f64) k_cloud<M_TEX>
+constexpr int kVerifyPipe = 2;  // ... of the verified-route k_cloud<M_VERIFY | M_TEX>
 static_assert(kWaves * kChunk >= 256 * kHistStride,
-              "k_cloud's pre-stats workgroups keep their LDS histogram replicas in s_ent (SLGPU_HIST_REP <= 14)");
-template <int MODE, int VEC, int PIPE = kPipe>
-__global__ __launch_bounds__(kThreads, PIPE > kPipe ? 1 : SLGPU_CLOUD_WAVES) void k_cloud(Params p) {
+              "k_cloud's pre-stats workgroups keep their LDS histogram replicas in s_ent");
+template <int MODE, int VEC, int PIPE>
+__global__ __launch_bounds__(kThreads, 5) void k_cloud(Params p) {
   __shared__ uint32_t s_ent[kWaves][kChunk];  // compacted points: pixel | code << 10
-  __shared__ __attribute__((aligned(16))) uint32_t s_bgr[kWaves][kBgrWords];  // colours (kBgrMode)
-  __shared__ float s_sxyz[kWaves][kStageOut ? 192 : 1];      // output stage: 64 points' xyz
-  __shared__ __attribute__((aligned(16))) uint8_t s_scol[kWaves][kStageOut ? 192 : kColDword ? kColStage : 4];  // colour bytes
+  __shared__ __attribute__((aligned(16))) uint32_t s_bgr[kWaves][kBgrWords];  // the chunks' colours
   __shared__ long long s_wred[kWaves];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
-  // pre-stats (sl_stack_next): S = gridDim.x - cloud_gx workgroups per view
-  // compute the next call's histograms, after the triangulating ones, or
-  // spread evenly among them (pre_mix: x is a pre-stats workgroup where
-  // floor(x S / T) steps)
-  int cx = blockIdx.x;  // triangulating workgroup index in the view
-  int64_t sx = -1;      // pre-stats workgroup index in the view
-  if (static_cast<int>(gridDim.x) > p.cloud_gx) {
-    const int64_t T = gridDim.x, S = T - p.cloud_gx, x = blockIdx.x;
-    if (p.pre_mix) {
-      const int64_t s0 = x * S / T, s1 = (x + 1) * S / T;
-      if (s1 != s0) sx = s0;
-      cx = static_cast<int>(x - s1);
-    } else if (x >= p.cloud_gx) {
-      sx = x - p.cloud_gx;
-    }
-  }
-  const int civ = cx * kWaves + wid;
-  if (sx >= 0) {
-    pre_stats_block(p, sx, gridDim.x - p.cloud_gx, &s_ent[0][0], reinterpret_cast<int*>(s_wred));
+  // pre-stats (sl_stack_next): the workgroups past cloud_gx compute the next
+  // call's (or launch group's) histograms, after the triangulating ones
+  const int cx = blockIdx.x;  // triangulating workgroup index in the view
+  if (cx >= p.cloud_gx) {
+    pre_stats_block(p, cx - p.cloud_gx, gridDim.x - p.cloud_gx, &s_ent[0][0], reinterpret_cast<int*>(s_wred));
     return;
   }
+  const int civ = cx * kWaves + wid;
   const int64_t b = static_cast<int64_t>(view) * p.cloud_gx + cx;  // block index in the launch
   const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
-  // (SLGPU_CLOUD_HOIST: the chunk's own loads before the offset's; measured slower)
-  ChunkIn in;
-  if (kCloudHoist && civ < p.cpv) cloud_load<VEC>(p, gc, lane, &in);
   const int before = (lane < wid && civ < p.cpv) ? p.chunk_counts[gc - wid + lane] : 0;  // earlier waves' chunks
-  long long base;
-  if (kAblate & 8192) {  // measurement only: no block prefix (disjoint slots of 1024 points)
-    base = static_cast<long long>(gc) * kChunk;
-  } else {
-    base = block_offset(p, b, tid, lane, wid, s_wred);
-    base += p.base_in ? *p.base_in : 0ll;
-    base += wave_sum(before);
-  }
+  long long base = block_offset(p, super_consume(p), b, tid, lane, wid, s_wred);
+  base += p.base_in ? *p.base_in : 0ll;
+  base += wave_sum(before);
   base = uniform64(base);
   if (civ >= p.cpv) return;
-  if (!kCloudHoist) cloud_load<VEC>(p, gc, lane, &in);
+  ChunkIn in;
+  cloud_load<VEC>(p, gc, lane, &in);
   if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1)
     p.view_offsets[p.n_views] = base + p.chunk_counts[gc];
-  cloud_chunk<MODE, VEC, PIPE>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0], &s_sxyz[wid][0], &s_scol[wid][0],
-                               kColDword && !kStageOut);
-}
-
-// ================================================================= k_fused ====
-// k_decode + k_cloud in one launch for calls of one launch group
-// (SLGPU_FUSED=1, measured A/B): every workgroup decodes its chunk group as
-// k_decode does (maps, mask, decision; no records), then, after a decoupled
-// look-back over the workgroups before it for its output offset, triangulates
-// its own points from registers -- the codes never leave the chip and one
-// kernel boundary goes.  The look-back waits only on lower-numbered
-// workgroups, dispatched before it and waiting on none after them, so it
-// completes whatever the residency (other calls in flight included); its
-// spin is bounded all the same (a give-up writes -1 as the call's total).
-// Granules (Params::lb): 8 bytes {tag, value}, stored and loaded whole at
-// agent scope -- the data is the flag (tag 1: the block's own count, 2: the
-// inclusive prefix) -- zeroed before the launch (k_stats, or a memset).
-__device__ __forceinline__ long long lookback_prefix(const Params& p, int64_t blk, unsigned own, int lane,
-                                                     bool* failed) {
-  unsigned long long* lb = p.lb;
-  if (lane == 0)
-    __hip_atomic_store(lb + blk, ((blk == 0 ? 2ull : 1ull) << 32) | own, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  *failed = false;
-  if (blk == 0) return 0;
-  long long acc = 0;
-  int64_t j = blk - 1;  // lane k reads block j - k
-  for (unsigned spins = 0;;) {
-    const int64_t jj = j - lane;
-    const unsigned long long g =
-        jj >= 0 ? __hip_atomic_load(lb + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (2ull << 32);
-    const unsigned tag = static_cast<unsigned>(g >> 32);
-    const unsigned long long incl = __ballot(tag == 2u);
-    const unsigned long long ready = __ballot(tag != 0u);
-    const int f = incl ? __builtin_ctzll(incl) : 63;  // the nearest inclusive prefix (or the whole window)
-    const unsigned long long need = f == 63 ? ~0ull : ((2ull << f) - 1ull);
-    if ((ready & need) == need) {
-      acc += wave_sum64(lane <= f ? static_cast<long long>(static_cast<unsigned>(g)) : 0ll);
-      if (incl) break;
-      j -= 64;
-      continue;
-    }
-    if (++spins > (1u << 22)) {  // never expected (see above): give up rather than hang
-      *failed = true;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  if (lane == 0)
-    __hip_atomic_store(lb + blk, (2ull << 32) | static_cast<unsigned>(acc + own), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  return acc;
-}
-
-template <int KC, int KR, int MODE, int CMODE, int PIPE>
-__global__ __launch_bounds__(kThreads, 2) void k_fused(Params p) {
-  __shared__ long long s_base;
-  __shared__ int s_wc[kWaves];
-  __shared__ int s_fail;
-  static_assert((MODE & M_FUSED) && (MODE & M_DECIDE) && (MODE & M_CODES), "k_fused: a decide-path cloud call");
-  static_assert(kWaves * (kChunk + kBgrWords) * 4 <= kDecodeLds, "the cloud's LDS fits in the decode tables'");
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  auto group = [&](const uint32_t* col, uint32_t pt, bool live, int n_px, int civ, int cg, unsigned* s_lds) {
-    const int view = blockIdx.y;
-    const int64_t px0 = static_cast<int64_t>(civ) * kChunk + lane * kPx;
-    const int64_t pxl = (live && n_px > 0) ? px0 : 0;
-    ChunkIn in;
-    // the colour first: its latency overlaps the look-back
-    if (p.tex != nullptr && kTexCoal) {  // cloud_load's 1-KB rows (cloud_chunk's LDS order)
-      const uint8_t* tb = p.tex + view * p.tex_vs;
-      const int64_t c0 = 3 * static_cast<int64_t>(civ) * kChunk + 16 * lane;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) in.tq[i] = ld_side16(tb + min<int64_t>(c0 + 1024 * i, 3 * p.HW - 16));
-    } else if (p.tex != nullptr) {
-      const uint8_t* t = p.tex + view * p.tex_vs + 3 * pxl;
-      in.tq[0] = ld_side16(t);
-      in.tq[1] = ld_side16(t + 16);
-      in.tq[2] = ld_side16(t + 32);
-    } else {
-      in.tq[0] = ld16(p.stack + view * p.stack_vs + pxl, n_px, true);
-      in.tq[1] = in.tq[2] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    const uint32_t cmax = static_cast<uint32_t>(p.Wp - 1);
-#pragma unroll
-    for (int i = 0; i < kPx / 2; ++i) in.d[i] = min(col[2 * i], cmax) | (min(col[2 * i + 1], cmax) << 16);
-    in.ptbits = (live && n_px == kPx) ? (pt & 0xffffu) : 0u;
-    const int cnt = wave_sum(__popc(in.ptbits));
-    if (lane == 0) s_wc[wid] = cnt;
-    __syncthreads();  // (also: every wave's decision is done with the LDS tables, reused below)
-    if (wid == 0) {
-      const int64_t blk = static_cast<int64_t>(view) * gridDim.x + cg;  // dispatch order
-      const unsigned own = static_cast<unsigned>(s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3]);
-      bool failed;
-      const long long pre = lookback_prefix(p, blk, own, lane, &failed);
-      if (lane == 0) {
-        s_base = pre + (p.base_in ? *p.base_in : 0ll);
-        s_fail = failed ? 1 : 0;
-      }
-    }
-    __syncthreads();
-    long long base = s_base;
-    for (int w = 0; w < wid; ++w) base += s_wc[w];
-    base = uniform64(base);
-    if (s_fail && tid == 0) p.view_offsets[p.n_views] = -1;  // (the give-up: an invalid total)
-    if (live) {
-      if (lane == 0 && view == p.n_views - 1 && civ == p.cpv - 1 && !s_fail) p.view_offsets[p.n_views] = base + cnt;
-      const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
-      uint32_t* s_ent = s_lds + wid * kChunk;
-      uint32_t* s_bgr = s_lds + kWaves * kChunk + wid * kBgrWords;
-      float dummy_xyz[1];
-      uint8_t dummy_col[4];
-      cloud_chunk<CMODE, 1, PIPE>(p, gc, base, lane, in, s_ent, s_bgr, dummy_xyz, dummy_col);
-    }
-  };
-  decode_body<KC, KR, MODE, 1>(p, group);
+  cloud_chunk<MODE, VEC, PIPE>(p, gc, base, lane, in, &s_ent[wid][0], &s_bgr[wid][0]);
 }
 
 }  // namespace
@@ -2777,47 +2152,46 @@ struct sl_ctx {
   double* d_planes = nullptr;  // [Wp] (n0, n1, n2, n.Oc + d)
   double* d_xn = nullptr;
   double* d_yn = nullptr;
-  float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H] | planes12 [Wp][3]
-  size_t off12 = 0;        // floats before planes12
+  float* d_f32 = nullptr;  // planes32 [Wp][4] | xn32 [W] | yn32 [H]
   float fast_thr = 0.0f;   // k_count's sufficient |n.r| threshold (Params::fast_thr)
   bool xy_safe = false;     // every xn / yn table entry is div_safe (Params::xy_safe)
-  bool xy_calc = false;     // xy_of reproduces every xn / yn entry (k_xy_check; SLGPU_XY_CALC=0: gathers, A/B)
+  bool xy_calc = false;     // xy_of reproduces every xn / yn entry (k_xy_check)
   bool xy_plain = false;    // every xn / yn entry has 2^-20 <= |v| <= 2^20 (the verified route's range premise)
   bool planes_plain = false;  // every plane has |w| >= 2^-500 and max|n_i| >= 2^-400 (ditto)
-  bool xy_calc_env = true;
   double cam[4] = {0, 0, 1, 1};  // cx, cy, fx, fy
-  bool verify32 = true;     // SL_XYZ_F32 by the verified shorter route (SLGPU_VERIFY32=0: the exact sequence, A/B)
+  bool verify32 = true;     // SL_XYZ_F32 by the verified shorter route (SLGPU_VERIFY32=0: the exact sequence,
+                            // a test switch: tests/test_gpu_parity.py compares the two)
   double* d_nc = nullptr;
   // scratch
   ViewStats* d_stats = nullptr;
   int64_t cap_stats = 0;
-  unsigned* d_hist[2] = {nullptr, nullptr};  // per-view histograms, parity double-buffered
-  int64_t cap_hist[2] = {0, 0};
-  int64_t hist_dirty[2] = {0, 0};  // leading views of each buffer that may be non-zero
-  int par = 0;                     // buffer the next adaptive launch accumulates into
+  // the adaptive mask's histograms: k_stats / pre-stats [view][kHistView], or
+  // k_decode's (3-kernel path) [view][kSlot]; zeroed by their consumer.  Two
+  // buffers: [0] for eager calls, [1] for calls captured into graphs -- a
+  // graph replays without the host, so eager calls never share its buffer
+  unsigned* d_hist[2] = {nullptr, nullptr};
+  int64_t cap_hist = 0;
+  int64_t hist_dirty[2] = {0, 0};  // leading words that may be non-zero (a queued pass, a failure)
+  unsigned long long cap_domain = 0;  // the capture whose calls the host tracked last in d_hist[1]
   int* d_chunk_counts = nullptr;
   int64_t cap_cc = 0;
   int* d_block_sums = nullptr;
   int64_t cap_bs = 0;
-  unsigned* d_super[2] = {nullptr, nullptr};  // super-block sums, parity double-buffered (kSuperCap each)
-  int spar = 0;
+  unsigned* d_super = nullptr;  // two super-block buffers (sums + dynamic-grid counters) + their selectors
+  bool super_dirty = false;     // a call stopped between k_decode / k_count and k_cloud: zeroed before the next
   uint8_t* d_ptnib = nullptr;
   int64_t cap_ptnib = 0;
   uint16_t* d_codes = nullptr;  // k_decode -> k_count / k_cloud records
   int64_t cap_codes = 0;
   int last_views = 0;
-  int decode_wgs = 0;  // k_decode grid cap in workgroups over all views (0: one workgroup per chunk group)
+  int decode_wgs = 0;  // k_decode grid cap in workgroups over all views
+  int pre_wgs = 0;     // pre-stats workgroups of a pass (8 per CU)
   // optional per-call HIP-event timing of k_decode / k_count / k_cloud
   std::vector<hipEvent_t> prof_ev;  // kProfEv events per call slot
   std::vector<int> prof_groups;     // launch groups recorded per call
   std::vector<char> prof_decide;    // per call: M_DECIDE path (events around k_stats, k_decode, k_cloud)
   int n_cu = 0;
-  bool force_3k = false;            // SLGPU_PATH=3: k_decode + k_count + k_cloud for aligned frames too (A/B)
-  bool rec_from_maps = false;       // maps + cloud: k_cloud reads the col map instead of the (12-bit)
-                                    // records (SLGPU_RECORDS=0; A/B: 1.6 % slower per step at config 2)
-  bool rec12 = true;                // cloud only: 12-bit packed records (SLGPU_REC12=0: 16-bit, A/B)
   int prof_n = 0;
-  // the last launch group's kernels and arguments (sl_time_kernels)
   // RCCL gather (sl_gather_init): communicator, this rank, count scratch
   void* comm = nullptr;
   int nranks = 0, rank = 0;
@@ -2830,60 +2204,27 @@ struct sl_ctx {
   bool done_valid = false;
   int64_t last_launches = 0, last_launch_px = 0;  // sl_last_launch_info
   int64_t* mc_next = nullptr;  // sl_mask_counts_to: the next sl_decode_triangulate's masked-pixel counts
-  // The adaptive mask's histogram pass (k_stats) ahead of its k_decode on a
-  // side stream, beside the previous launch group's k_cloud: for the later
-  // launch groups of a call, and for a call's first group when the caller
-  // declared the stack ready (sl_stack_ready).  Its only scratch is the
-  // parity-buffered histograms, so it waits for no more than the last kernel
-  // that read them (hist_ev) and the caller's readiness event.
-  hipStream_t side = nullptr;
-  hipEvent_t hist_ev = nullptr;   // after the latest kernel that reads the histograms (k_decode / k_count)
-  hipEvent_t stats_ev = nullptr;  // after a k_stats on `side` (its k_decode waits for it)
-  hipEvent_t entry_ev = nullptr;  // the side path's first use: everything queued before it
-  bool hist_tracked = false;      // hist_ev is recorded after every histogram reader from now on
-  bool ready_next = false;        // sl_stack_ready: armed for the next sl_decode_triangulate
+  bool ready_next = false;     // sl_stack_ready: armed for the next sl_decode_triangulate
   hipEvent_t ready_ev_next = nullptr;
-  bool no_side = false;           // SLGPU_STATS_SIDE=0: k_stats always on the call's stream (A/B)
-  bool fused = false;             // SLGPU_FUSED=1: k_fused for one-group cloud calls (A/B)
-  unsigned long long* d_lb = nullptr;  // k_fused's look-back granules
-  int64_t cap_lb = 0;
-  bool side_groups = false;       // SLGPU_STATS_SIDE=1: also the later launch groups of every call (A/B;
-                                  // off by default: a cross-stream event wait measured 10-20 us of latency,
-                                  // more than the k_stats it hides)
   // Pre-stats (sl_stack_next): a call's last k_cloud also runs the histogram
-  // pass of the NEXT call's first launch group (declared stack), so that call
-  // starts with its k_decode.  Three buffers in rotation: the one the current
-  // call's k_decode reads, the one its k_cloud accumulates into, and the one
-  // that k_cloud zeroes for the following pass (last read a call earlier).
-  unsigned* d_pre[3] = {nullptr, nullptr, nullptr};
-  int64_t cap_pre = 0;                // words of each
-  int64_t pre_dirty[3] = {0, 0, 0};   // leading words that may be non-zero
-  int pre_acc = 0;                    // buffer the next pre-stats pass accumulates into
+  // pass of the NEXT call's first launch group (declared stack) into d_hist,
+  // so that call starts with its k_decode.
   bool decl_next = false;             // sl_stack_next armed for the coming call
   const uint8_t* decl_stack = nullptr;
   int64_t decl_vs = 0;
   int decl_views = 0;
-  bool pre_armed = false;             // a pre-stats pass was queued for the next call
-  int pre_buf = 0;                    // ... into this buffer
-  const uint8_t* pre_stack = nullptr; // ... of this stack, stride, first-group views, frame
+  bool pre_armed = false;             // a pass was queued for the next call: of this stack, stride, views, frame
+  const uint8_t* pre_stack = nullptr;
   int64_t pre_vs = 0, pre_hw = 0;
   int pre_views = 0;
-  bool no_pre = false;                // SLGPU_PRESTATS=0: sl_stack_next ignored, no pre-stats at all (A/B)
-  bool no_pre_groups = false;         // SLGPU_PRE_GROUPS=0: no pre-stats between a call's launch groups (A/B)
-  int pre_mix = 0;                    // SLGPU_PRE_MIX=1: pre-stats workgroups spread among k_cloud's (A/B)
-  int pre_wgs = 0;                    // SLGPU_PRE_WGS=n: pre-stats workgroups in all (A/B; 0: 8 per CU)
-  bool pre_decode = false;            // SLGPU_PRE_DECODE=1: pre-stats workgroups in k_decode's tail (A/B)
-  int64_t max_chunks = kMaxChunks;    // chunks per launch group (SLGPU_GROUP_CHUNKS=n, at most kMaxChunks: A/B)
-  int decode_dyn = -1;                // k_decode's later rounds pulled dynamically: -1 cloud-only calls (no
-                                      // maps), SLGPU_DECODE_DYN=0 never, =1 every cloud call (A/B)
-  bool decode_balance = false;        // SLGPU_DECODE_BALANCE=1: the capped k_decode grid shrunk so that every
-                                      // workgroup decodes the same number of chunk groups (A/B)
+  unsigned long long pre_capture = 0;  // ... queued inside this stream capture (capture id + 1; 0: eagerly)
+  // the last launch group's kernels and arguments (sl_time_kernels)
   struct {
     bool valid = false;
     bool decide = false;  // fn[1] = k_stats (or null) instead of k_count
-    bool fused = false;   // fn[0] = k_fused (decode and cloud), fn[2] = null
+    bool stats = false;   // decide, adaptive: p[1] / grid[1] are k_stats' (to rebuild the histograms)
     Params p[3];
-    const void* fn[3] = {nullptr, nullptr, nullptr};  // k_decode, k_count, k_cloud (or null)
+    const void* fn[3] = {nullptr, nullptr, nullptr};  // k_decode, k_count / k_stats (or null), k_cloud (or null)
     dim3 grid[3];
     hipStream_t s = nullptr;
   } last;
@@ -2978,8 +2319,11 @@ int grow(sl_ctx* c, T** ptr, int64_t* cap, int64_t need) {
   return SL_OK;
 }
 
-// scratch for `views` views of `px` pixels each
-int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes) {
+// scratch for `views` views of `px` pixels each (histograms: for
+// max(views, hist_views)); *hist_fresh: the histogram buffer was
+// (re)allocated (zeroed: a pass queued in it is gone)
+int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes, int64_t hist_views = 0,
+                   bool* hist_fresh = nullptr) {
   const int64_t chunks = views * ((px + kChunk - 1) / kChunk);
   int r = grow(c, &c->d_chunk_counts, &c->cap_cc, chunks);
   if (r) return r;
@@ -2987,18 +2331,22 @@ int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes) {
   if (r) return r;
   r = grow(c, &c->d_ptnib, &c->cap_ptnib, chunks * kChunkNib);
   if (r) return r;
-  for (int b = 0; b < 2; ++b) {
-    int64_t cap = c->d_super[b] ? kSuperCap : 0;
-    r = grow(c, &c->d_super[b], &cap, kSuperCap);  // zeroed once; then by the kernels
+  int64_t scap = c->d_super ? kSuperWords : 0;
+  r = grow(c, &c->d_super, &scap, kSuperWords);  // zeroed once; then by the kernels (super_produce)
+  if (r) return r;
+  const int64_t before = c->cap_hist, need = std::max(views, hist_views) * kHistView;
+  for (int d = 0; d < 2; ++d) {  // k_stats' replicas (k_decode's: kSlot)
+    int64_t cap = before;
+    r = grow(c, &c->d_hist[d], &cap, need);
     if (r) return r;
+    if (d == 1) c->cap_hist = cap;
   }
-  for (int b = 0; b < 2; ++b) {
-    const int64_t before = c->cap_hist[b];
-    r = grow(c, &c->d_hist[b], &c->cap_hist[b], views * kHistView);  // k_stats' replicas (k_decode's: kSlot)
-    if (r) return r;
-    if (c->cap_hist[b] != before) c->hist_dirty[b] = 0;  // fresh (zeroed) allocation
+  if (c->cap_hist != before) {
+    c->hist_dirty[0] = c->hist_dirty[1] = 0;
+    c->pre_armed = false;
+    if (hist_fresh) *hist_fresh = true;
   }
-  // (u16 units: 2 B/px, or kRecBlk's 1536-B slots of whole chunk groups)
+  // (u16 units: 2 B/px, or the 1536-B slots of whole chunk groups)
   if (codes)
     return grow(c, &c->d_codes, &c->cap_codes,
                 std::max<int64_t>(views * px, views * ((px + 4 * kChunk - 1) / (4 * kChunk)) * 4 * (kRecSlot / 2)) + 16);
@@ -3010,19 +2358,13 @@ constexpr int kProfGroups = 64;            // launch groups timed per call (at m
 constexpr int kProfEv = 4 * kProfGroups;   // events per call: per group before k_decode, k_count, k_cloud, after
                                            // (M_DECIDE: before k_stats, k_decode, k_cloud, after)
 
-// k_decode specialisations for the benchmark configurations; everything else
-// (other bit counts, unaligned frames) runs the generic instantiation.
+// k_decode specialisations for the benchmark configurations (the decide
+// path); everything else (other bit counts, the 3-kernel path of unaligned or
+// very large frames) runs the generic instantiation.
 KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
   if (vec && !(mode & (M_NC | M_FROMMAPS))) {
     constexpr int mrch = M_MAPS | M_ROWS | M_CODES | M_HIST, mrh = M_MAPS | M_ROWS | M_HIST,
                   ch = M_CODES | M_HIST, mrc = M_MAPS | M_ROWS | M_CODES, cc = M_CODES;
-    if (mode == mrch && kc == 11 && kr == 11) return k_decode<11, 11, mrch, 1>;
-    if (mode == mrch && kc == 10 && kr == 0) return k_decode<10, 0, mrch, 1>;
-    if (mode == mrh && kc == 11 && kr == 11) return k_decode<11, 11, mrh, 1>;
-    if (mode == ch && kc == 11) return k_decode<11, 0, ch, 1>;
-    if (mode == ch && kc == 10) return k_decode<10, 0, ch, 1>;
-    if (mode == mrc && kc == 11 && kr == 11) return k_decode<11, 11, mrc, 1>;
-    if (mode == cc && kc == 11) return k_decode<11, 0, cc, 1>;
     constexpr int D = M_DECIDE;
     if (mode == (mrch | D) && kc == 11 && kr == 11) return k_decode<11, 11, mrch | D, 1>;
     if (mode == (mrch | D) && kc == 10 && kr == 0) return k_decode<10, 0, mrch | D, 1>;
@@ -3041,42 +2383,14 @@ KernelFn pick_decode(int kc, int kr, int mode, bool vec) {
   return vec ? k_decode<-1, -1, -1, 1> : k_decode<-1, -1, -1, 0>;
 }
 
-KernelFn pick_cloud(int mode, bool vec, bool small) {
-  if (vec && small && kSmallPipe > kPipe && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1, kSmallPipe>;
+KernelFn pick_cloud(int mode, bool vec) {
   if (vec && mode == M_TEX) return k_cloud<M_TEX, 1, kExactPipe>;  // f32 xyz, pinhole rays, BGR texture
   if (vec && mode == (M_VERIFY | M_TEX)) return k_cloud<M_VERIFY | M_TEX, 1, kVerifyPipe>;  // ... verified route
-  if (vec && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1>;
+  if (vec && mode == (M_FAST32 | M_TEX)) return k_cloud<M_FAST32 | M_TEX, 1, kPipe>;
   return vec ? k_cloud<-1, 1, kExactPipe> : k_cloud<-1, 0, kExactPipe>;  // (f64 chains: kExactPipe points per pass)
 }
 
-// k_fused instantiations: the benchmark configurations' one-group calls
-// (decode mode with M_DECIDE | M_FUSED, cloud mode), else null
-KernelFn pick_fused(int kc, int kr, int dmode, int cmode) {
-  constexpr int D = M_DECIDE | M_FUSED, mrch = M_MAPS | M_ROWS | M_CODES | M_HIST, ch = M_CODES | M_HIST;
-  constexpr int V = M_VERIFY | M_TEX, F = M_FAST32 | M_TEX;
-  if (dmode == (mrch | D) && kc == 10 && kr == 0 && cmode == V) return k_fused<10, 0, mrch | D, V, kVerifyPipe>;
-  if (dmode == (mrch | D) && kc == 11 && kr == 11 && cmode == V) return k_fused<11, 11, mrch | D, V, kVerifyPipe>;
-  if (dmode == (mrch | D) && kc == 11 && kr == 11 && cmode == F) return k_fused<11, 11, mrch | D, F, kPipe>;
-  if (dmode == (ch | D) && kc == 11 && cmode == V) return k_fused<11, 0, ch | D, V, kVerifyPipe>;
-  return nullptr;
-}
-
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
-// Enqueue, per launch group of views, k_decode -> k_count [-> k_cloud] on
-// stream s -- or, when decode_mode has M_DECIDE, [k_stats ->] k_decode
-// [-> k_cloud] (k_decode applies the mask and makes the point decision).
-// decode_mode / count_mode / cloud_mode (< 0: no cloud) are the kernels' mode
-// bits.  Launch groups hold at most kMaxChunks chunks (at least one view); a
-// group's points follow the earlier groups' (base_in).
-// The side stream and its events (created on first use).
-int ensure_side(sl_ctx* c) {
-  if (c->side) return SL_OK;
-  for (hipEvent_t* e : {&c->hist_ev, &c->stats_ev, &c->entry_ev})
-    if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
-  HIP_TRY(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-  return SL_OK;
-}
 
 // The one-call arms of a context (sl_stack_next's declaration, the pre-stats
 // pass an earlier call queued): taken -- and cleared on the context -- at the
@@ -3096,104 +2410,124 @@ PreArms take_arms(sl_ctx* c) {
   return a;
 }
 
-// ready: the caller declared the stack ready (sl_stack_ready; ready_ev, if
-// non-null, completes when it is): the first launch group's k_stats may run on
-// the side stream too.
-int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mode, int cloud_mode,
-           hipStream_t s, PreArms arms, bool ready = false, hipEvent_t ready_ev = nullptr) {
+// Zero n words at p on stream s.  A kernel, not hipMemsetAsync: captured into
+// a hipGraph, a memset node of the histogram buffer left garbage in it from
+// the graph's second replay on (measured: scripts/dbg/graph1b.py; the kernel
+// and no clear at all both replay bit-exactly).
+__global__ __launch_bounds__(256) void k_zero(unsigned* p, int64_t n) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += 256ll * gridDim.x) p[i] = 0u;
+}
+int zero_async(sl_ctx* c, void* p, int64_t words, hipStream_t s) {
+  if (words <= 0) return SL_OK;
+  const unsigned blocks = static_cast<unsigned>(std::min<int64_t>((words + 255) / 256, 1024));
+  hipLaunchKernelGGL(k_zero, dim3(blocks), dim3(256), 0, s, static_cast<unsigned*>(p), words);
+  HIP_TRY(c, hipGetLastError());
+  return SL_OK;
+}
+// The stream capture `s` is in: its id + 1, or 0 when it is not capturing.
+int capture_of(sl_ctx* c, hipStream_t s, unsigned long long* out) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  HIP_TRY(c, hipStreamGetCaptureInfo(s, &st, &id));
+  *out = st == hipStreamCaptureStatusActive ? id + 1 : 0;
+  return SL_OK;
+}
+
+// Enqueue, per launch group of views, k_decode -> k_count [-> k_cloud] on
+// stream s -- or, when decode_mode has M_DECIDE, [k_stats ->] k_decode
+// [-> k_cloud] (k_decode applies the mask and makes the point decision).
+// decode_mode / count_mode / cloud_mode (< 0: no cloud) are the kernels' mode
+// bits.  Launch groups hold at most kMaxChunks chunks (at least one view); a
+// group's points follow the earlier groups' (base_in).
+//
+// Scratch at every launch-group boundary: the super-block buffer is zero (its
+// consumer, k_cloud, zeroes it) and so is the histogram buffer (k_decode /
+// k_count zero what they read), except that it may hold one queued pre-stats
+// pass for the next group or call.  A call takes a queued pass only when it
+// is of its first group's stack, stride, views and frame AND was queued in
+// the same stream capture (or both eagerly): a captured graph never depends
+// on a pass queued outside it, so it replays in any phase, any number of
+// times.  A pass not taken is cleared (a memset on the stream) before the
+// buffer is used again; so is anything a failed call left behind.
+int launch_groups(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mode, int cloud_mode,
+                  hipStream_t s, PreArms arms) {
   const bool decide = (decode_mode & M_DECIDE) != 0;
+  const bool codes = (decode_mode & M_CODES) != 0;
   const int64_t cpv = p0.cpv;
-  const int vpg = static_cast<int>(std::max<int64_t>(1, c->max_chunks / cpv));  // views per group
+  const int vpg = static_cast<int>(std::max<int64_t>(1, kMaxChunks / cpv));  // views per group
   const int n_groups = static_cast<int>((p0.n_views + vpg - 1) / vpg);
   const bool adaptive = (decode_mode & M_HIST) != 0;
-  // k_stats on the side stream (never while `s` is being captured into a
-  // graph: the side path waits on events recorded outside the capture)
-  bool side_ok = false;
-  if (decide && adaptive && c->prof_ev.empty() && (ready || (n_groups > 1 && c->side_groups)) && !c->no_side) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    HIP_TRY(c, hipStreamIsCapturing(s, &cs));
-    side_ok = cs == hipStreamCaptureStatusNone;
-    if (side_ok) {
-      int r = ensure_side(c);
-      if (r) return r;
-    }
-  }
-  int r = ensure_scratch(c, std::min(vpg, p0.n_views), p0.HW, (decode_mode & M_CODES) != 0);
+  const bool pre_run = arms.decl && cloud_mode >= 0 && vec;
+  bool hist_fresh = false;
+  int r = ensure_scratch(c, std::min(vpg, p0.n_views), p0.HW, codes, pre_run ? std::min(vpg, c->decl_views) : 0,
+                         &hist_fresh);
   if (r) return r;
   r = grow(c, &c->d_stats, &c->cap_stats, p0.n_views);
   if (r) return r;
+  unsigned long long cap_id = 0;
+  r = capture_of(c, s, &cap_id);
+  if (r) return r;
   // Pre-stats (sl_stack_next): this call's first group takes the histograms
-  // the previous call's k_cloud computed for it (same stack, stride, views
-  // and frame), and this call's last k_cloud computes those of the call
-  // declared next.  (Not with k_fused, whose look-back granules k_stats zeroes.)
+  // the previous call's k_cloud computed for it, and this call's last k_cloud
+  // computes those of the call declared next.
   const int nv0 = std::min(vpg, p0.n_views);
-  bool pre_use = arms.armed && decide && adaptive && !c->fused && p0.stack == c->pre_stack &&
-                 p0.stack_vs == c->pre_vs && nv0 == c->pre_views && p0.HW == c->pre_hw;
-  int pre_in = c->pre_buf;
-  const bool pre_run = arms.decl && !c->no_pre && !c->fused && cloud_mode >= 0 && vec;
-  const bool pre_dec = pre_run && decide && c->pre_decode;  // ... in the last k_decode instead (A/B)
+  const bool pre_use = arms.armed && !hist_fresh && decide && adaptive && p0.stack == c->pre_stack &&
+                       p0.stack_vs == c->pre_vs && nv0 == c->pre_views && p0.HW == c->pre_hw &&
+                       c->pre_capture == cap_id;
   // Within a call of several launch groups: group g's k_cloud also runs group
   // g + 1's histogram pass (the same pre-stats workgroups), so only the first
-  // group can need a k_stats launch (SLGPU_PRE_GROUPS=0: every group its own, A/B)
-  const bool pre_groups = decide && adaptive && n_groups > 1 && !c->no_pre && !c->no_pre_groups && !c->fused &&
-                          cloud_mode >= 0 && vec;
-  // pre-stats workgroups per view of a pass over nv views: up to 8 per CU in
-  // all (one 16-pixel step per thread at config 2; measured 0.5-1 us faster
-  // per c2 step than k_stats' 2 per CU)
+  // group can need a k_stats launch.
+  const bool pre_groups = decide && adaptive && n_groups > 1 && cloud_mode >= 0 && vec;
+  // eager calls and captured calls keep their histograms apart: a graph's
+  // replays change its buffer without the host, so the first call of every
+  // capture takes that buffer as dirty (later calls of the capture follow it)
+  const int dom = cap_id ? 1 : 0;
+  unsigned* const hbuf = c->d_hist[dom];
+  int64_t& hist_dirty = c->hist_dirty[dom];
+  if (dom == 1 && c->cap_domain != cap_id) {
+    c->cap_domain = cap_id;
+    hist_dirty = c->cap_hist;
+  }
+  // what the stream's scratch may still hold: clear it before anything reads or accumulates
+  if (c->super_dirty) {
+    r = zero_async(c, c->d_super, kSuperWords, s);
+    if (r) return r;
+  }
+  c->super_dirty = false;
+  if (!pre_use && hist_dirty > 0) {
+    r = zero_async(c, hbuf, hist_dirty, s);
+    if (r) return r;
+  }
+  if (!pre_use) hist_dirty = 0;
+  // pre-stats workgroups per view of a pass over nv views: 8 per CU in all
+  // (one 16-pixel step per thread at config 2; measured 0.5-1 us faster per c2
+  // step than k_stats' 2 per CU)
   auto pre_bpv_of = [&](int nv) -> int64_t {
     const int64_t per_view = (p0.HW / 16 + kThreads - 1) / kThreads;
-    const int64_t wgs = c->pre_wgs > 0 ? c->pre_wgs : 8 * c->n_cu;
-    return std::max<int64_t>(1, std::min<int64_t>(per_view, (wgs + nv - 1) / nv));
+    return std::max<int64_t>(1, std::min<int64_t>(per_view, (c->pre_wgs + nv - 1) / nv));
   };
-  {
-    int64_t words = 0;
-    if (pre_run) words = static_cast<int64_t>(std::min(vpg, c->decl_views)) * kHistView;
-    if (pre_groups) words = std::max<int64_t>(words, static_cast<int64_t>(std::min(vpg, p0.n_views - vpg)) * kHistView);
-    if (words > c->cap_pre) {  // (re)allocated zeroed: nothing left to take
-      pre_use = false;
-      for (int b = 0; b < 3; ++b) {
-        int64_t cap = c->cap_pre;
-        r = grow(c, &c->d_pre[b], &cap, words);
-        if (r) return r;
-        if (b == 2) c->cap_pre = cap;
-        c->pre_dirty[b] = 0;
-      }
-    }
-  }
   c->last_views = p0.n_views;
-  if (p0.masked)  // the caller's per-view counts, accumulated by the groups' k_decode / k_count
-    HIP_TRY(c, hipMemsetAsync(p0.masked, 0, sizeof(unsigned long long) * p0.n_views, s));
+  if (p0.masked) {  // the caller's per-view counts, accumulated by the groups' k_decode / k_count
+    r = zero_async(c, p0.masked, 2 * static_cast<int64_t>(p0.n_views), s);
+    if (r) return r;
+  }
   hipEvent_t* ev = nullptr;
   if (!c->prof_ev.empty() && kProfEv * (c->prof_n + 1) <= static_cast<int>(c->prof_ev.size()))
     ev = &c->prof_ev[kProfEv * c->prof_n++];
   // The pre-stats workgroups' arguments on launch parameters pc of a grid
   // with nv rows, for the pnv views of stack pst (view stride pvs): the launch
   // grows by as many workgroups per row as they need (after its own); the
-  // pass accumulates into buffer c->pre_buf, for the stack recorded in c->pre_*.
-  auto add_pre = [&](Params& pc, dim3& grid, int nv, const uint8_t* pst, int64_t pvs, int pnv) -> int {
-    const int acc = c->pre_acc, zb = (acc + 1) % 3;
+  // pass accumulates into the (clean) histogram buffer.
+  auto add_pre = [&](Params& pc, dim3& grid, int nv, const uint8_t* pst, int64_t pvs, int pnv) {
     const int64_t bpv = pre_bpv_of(pnv);
-    if (c->pre_dirty[acc] > 0)
-      HIP_TRY(c, hipMemsetAsync(c->d_pre[acc], 0, sizeof(unsigned) * c->pre_dirty[acc], s));
     pc.pre_stack = pst;
     pc.pre_vs = pvs;
-    pc.pre_hist = c->d_pre[acc];
-    pc.pre_zero = c->d_pre[zb];
-    pc.pre_zero_words = c->pre_dirty[zb];
+    pc.pre_hist = hbuf;
     pc.pre_views = pnv;
     pc.pre_bpv = static_cast<int>(bpv);
-    pc.pre_mix = c->pre_mix;
     const int64_t total = static_cast<int64_t>(pnv) * bpv;
     grid.x += static_cast<unsigned>((total + nv - 1) / nv);
-    c->pre_dirty[acc] = static_cast<int64_t>(pnv) * kHistView;
-    c->pre_dirty[zb] = 0;
-    c->pre_acc = zb;
-    c->pre_buf = acc;
-    c->pre_stack = pst;
-    c->pre_vs = pvs;
-    c->pre_views = pnv;
-    c->pre_hw = p0.HW;
-    return SL_OK;
+    hist_dirty = static_cast<int64_t>(pnv) * kHistView;
   };
   bool next_pre = pre_use;  // the coming group's histograms were computed by the previous k_cloud
   int g = 0;  // launch group index
@@ -3218,142 +2552,74 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
     p.base_in = (v0 > 0 && p.view_offsets) ? p.view_offsets : nullptr;
     p.stats = c->d_stats + v0;
     p.codes = c->d_codes;
-    // maps + cloud on the decide path: k_cloud reads the col map (no records)
-    p.rec_col = (decide && p.col_out && cloud_mode >= 0 && c->rec_from_maps) ? p.col_out : nullptr;
-    p.rec12 = (decide && vec && !p.rec_col && cloud_mode >= 0 && p.Wp < 4096 && c->rec12) ? 1 : 0;
-    p.rec_blk = (p.rec12 && kRecBlk && (!(decode_mode & M_MAPS) || SLGPU_REC_BLK_MAPS)) ? 1 : 0;  // (k_decode's `blk`)
+    // the decide path's records are 12 bits (Wp <= kDecPl): chunk slots for
+    // cloud-only calls, pixel order with maps (k_decode's `blk`)
+    p.rec12 = (decide && cloud_mode >= 0) ? 1 : 0;
+    p.rec_blk = (p.rec12 && !(decode_mode & M_MAPS)) ? 1 : 0;
     p.ptnib = c->d_ptnib;
     p.chunk_counts = c->d_chunk_counts;
     p.block_sums = c->d_block_sums;
-    // this group's k_stats on the side stream: after the last reader of the
-    // histograms it zeroes (the previous group's or call's k_decode) and, for
-    // a call's first group, the caller's readiness event (else after
-    // everything queued so far: the side path's first use)
+    p.hist = hbuf;
+    p.super_base = c->d_super;
+    p.super_par = c->d_super + 2 * kSuperCap;
     const bool pre_g = next_pre;  // histograms computed by the previous k_cloud (this call's or the last call's)
     next_pre = false;
-    const bool ahead = !pre_g && side_ok && ((g > 0 && c->side_groups) || (g == 0 && ready));
-    hipStream_t ss = ahead ? c->side : s;
-    if (g == 0 && ready_ev && !ahead) HIP_TRY(c, hipStreamWaitEvent(s, ready_ev, 0));  // the promise, kept on s
-    if (ahead) {
-      if (g == 0 && ready_ev) HIP_TRY(c, hipStreamWaitEvent(ss, ready_ev, 0));
-      if (!c->hist_tracked) {
-        HIP_TRY(c, hipEventRecord(c->entry_ev, s));
-        HIP_TRY(c, hipStreamWaitEvent(ss, c->entry_ev, 0));
-        c->hist_tracked = true;
-      } else {
-        HIP_TRY(c, hipStreamWaitEvent(ss, c->hist_ev, 0));
-      }
-    }
-    if (pre_g) {
-      p.hist = c->d_pre[pre_in];
-      p.hist_zero = nullptr;
-    } else if (adaptive) {  // hist_dirty: leading words of a buffer that may be non-zero
-      const int a = c->par, b = 1 - c->par;
-      const int64_t words = static_cast<int64_t>(nv) * (decide ? kHistView : kSlot);
-      if (c->hist_dirty[a] > 0)
-        HIP_TRY(c, hipMemsetAsync(c->d_hist[a], 0, sizeof(unsigned) * c->hist_dirty[a], ss));
-      p.hist = c->d_hist[a];
-      p.hist_zero = c->d_hist[b];
-      c->hist_dirty[a] = words;  // accumulated now; this launch zeroes b's leading `words`
-      if (c->hist_dirty[b] <= words) c->hist_dirty[b] = 0;
-      c->par = b;
-    }
     const dim3 grid(static_cast<unsigned>((cpv + kWaves - 1) / kWaves), static_cast<unsigned>(nv));
     {  // super-block size: the smallest power of two >= sqrt(blocks of the group)
       const int64_t nb = static_cast<int64_t>(grid.x) * nv;
       int sh = 0;
       while ((int64_t{1} << (2 * sh)) < nb) ++sh;
       p.sb_shift = sh;
-      p.super_sums = c->d_super[c->spar];
-      p.super_zero = c->d_super[c->spar ^ 1];
-      p.super_cap = kSuperCap;
-      c->spar ^= 1;
     }
     c->last.valid = true;
     dim3 dgrid = grid;  // k_decode: chunk groups strided over a capped grid
     if (c->decode_wgs > 0) dgrid.x = std::min(grid.x, static_cast<unsigned>(std::max(1, (c->decode_wgs + nv - 1) / nv)));
-    if (c->decode_balance) {  // rounds of the capped grid, and the fewest workgroups that need no more
-      const unsigned rounds = (grid.x + dgrid.x - 1) / dgrid.x;
-      dgrid.x = (grid.x + rounds - 1) / rounds;
-    }
     c->last.grid[0] = dgrid;
     // barrier-free block sums when every k_decode workgroup iterates at most
     // kBsSlots chunk groups (4 chunks of at most 1024 points: 16-bit sums)
     p.bs_atomic = decide && (grid.x + dgrid.x - 1) / dgrid.x <= static_cast<unsigned>(kBsSlots);
-    // decode_dyn (cloud-only calls; SLGPU_DECODE_DYN): a capped decode grid pulls its chunk
-    // groups after the first round from per-view counters (the last entries of
-    // this launch's super-block buffer, zeroed with it); block sums then take
-    // the barrier path, whose barrier publishes each workgroup's next group
-    const bool dyn_want = c->decode_dyn > 0 || (c->decode_dyn < 0 && !(decode_mode & M_MAPS));
-    p.decode_dyn = (dyn_want && decide && (decode_mode & M_CODES) && dgrid.x < grid.x &&
+    // cloud-only calls: a capped decode grid pulls its chunk groups after the
+    // first round from per-view counters (the last entries of the super-block
+    // buffer); block sums then take the barrier path, whose barrier publishes
+    // each workgroup's next group.  (On maps calls measured slower: c2 119.4
+    // -> 122.0-122.6 us)
+    p.decode_dyn = (!(decode_mode & M_MAPS) && decide && codes && dgrid.x < grid.x &&
                     ((static_cast<int64_t>(grid.x) * nv) >> p.sb_shift) + 1 + nv < kSuperCap) ? 1 : 0;
     if (p.decode_dyn) p.bs_atomic = 0;
     c->last.grid[1] = c->last.grid[2] = grid;
     c->last.s = s;
-    c->last.fn[2] = nullptr;
+    c->last.fn[1] = c->last.fn[2] = nullptr;
     c->last.decide = decide;
-    // k_fused (SLGPU_FUSED=1): a one-group cloud call's decode and cloud in
-    // one launch; its look-back granules zeroed by k_stats (or a memset)
-    KernelFn fusedfn = nullptr;
-    if (c->fused && decide && vec && cloud_mode >= 0 && n_groups == 1)
-      fusedfn = pick_fused(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode | M_FUSED, cloud_mode);
-    c->last.fused = fusedfn != nullptr;
-    if (fusedfn) {
-      r = grow(c, &c->d_lb, &c->cap_lb, static_cast<int64_t>(grid.x) * nv);
-      if (r) return r;
-      p.lb = c->d_lb;
-      p.lb_n = static_cast<int64_t>(grid.x) * nv;
-      if (!adaptive) HIP_TRY(c, hipMemsetAsync(c->d_lb, 0, sizeof(unsigned long long) * p.lb_n, s));
-    }
+    c->last.stats = false;
     if (decide) {
-      c->last.fn[1] = nullptr;
-      if (adaptive && !pre_g) {  // k_stats: the thresholds' histograms, before the decode applies them
+      if (adaptive) {  // k_stats' launch (or what would rebuild the histograms for sl_time_kernels)
         const int64_t per_view = (p0.HW / 16 + kThreads - 1) / kThreads;
         const dim3 sg(static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>(per_view, (2 * c->n_cu + nv - 1) / nv))),
                       static_cast<unsigned>(nv));
         p.mode = decode_mode;
-        void* args[] = {&p};
         c->last.p[1] = p;
-        const void* kst = reinterpret_cast<const void*>(k_stats);
-        c->last.fn[1] = kst;
         c->last.grid[1] = sg;
-        HIP_TRY(c, hipLaunchKernel(kst, sg, dim3(kThreads), args, 0, ss));
-        if (ahead) {
-          HIP_TRY(c, hipEventRecord(c->stats_ev, ss));
-          HIP_TRY(c, hipStreamWaitEvent(s, c->stats_ev, 0));
+        c->last.stats = true;
+        if (!pre_g) {  // k_stats: the thresholds' histograms, before the decode applies them
+          void* args[] = {&p};
+          const void* kst = reinterpret_cast<const void*>(k_stats);
+          c->last.fn[1] = kst;
+          HIP_TRY(c, hipLaunchKernel(kst, sg, dim3(kThreads), args, 0, s));
         }
       }
       if (gev) HIP_TRY(c, hipEventRecord(gev[1], s));
     }
-    if (fusedfn) {  // one workgroup per chunk group (uncapped grid), then its cloud
-      p.mode = decode_mode | M_FUSED;
-      p.bs_atomic = 0;
-      void* args[] = {&p};
-      c->last.p[0] = p;
-      c->last.p[0].masked = nullptr;
-      c->last.fn[0] = reinterpret_cast<const void*>(fusedfn);
-      c->last.grid[0] = grid;
-      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fusedfn), grid, dim3(kThreads), args, 0, s));
-    } else {
+    if (codes) c->super_dirty = true;  // until this group's k_cloud is enqueued
+    {
       p.mode = decode_mode;
       KernelFn fn = pick_decode(p.kc, (decode_mode & M_ROWS) ? p.kr : 0, decode_mode, vec);
       c->last.p[0] = p;
       c->last.p[0].masked = nullptr;  // sl_time_kernels' re-runs leave the caller's counts alone
       c->last.fn[0] = reinterpret_cast<const void*>(fn);
-      Params pd = p;
-      dim3 pgrid = dgrid;
-      if (pre_dec && g == n_groups - 1) {  // + the declared next call's histogram pass, in k_decode's tail
-        pd.decode_gx = static_cast<int>(dgrid.x);
-        r = add_pre(pd, pgrid, nv, c->decl_stack, c->decl_vs, std::min(vpg, c->decl_views));
-        if (r) return r;
-      }
-      void* args[] = {&pd};
-      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), pgrid, dim3(kThreads), args, 0, s));
-      if (pre_dec && g == n_groups - 1) c->pre_armed = true;
-    }
-    if (adaptive && decide && (c->hist_tracked || (side_ok && c->side_groups && g + 1 < n_groups))) {
-      HIP_TRY(c, hipEventRecord(c->hist_ev, s));  // the last reader of this group's histograms
-      c->hist_tracked = true;
+      void* args[] = {&p};
+      HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), dgrid, dim3(kThreads), args, 0, s));
+      // 3-kernel path, adaptive: k_decode accumulates the histograms k_count consumes
+      hist_dirty = (adaptive && !decide) ? static_cast<int64_t>(nv) * kSlot : 0;
     }
     if (gev) HIP_TRY(c, hipEventRecord(gev[decide ? 2 : 1], s));
     if (!decide) {
@@ -3364,36 +2630,37 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
       c->last.p[1].masked = nullptr;
       c->last.fn[1] = fn;
       HIP_TRY(c, hipLaunchKernel(fn, grid, dim3(kThreads), args, 0, s));
-      if (adaptive && c->hist_tracked) HIP_TRY(c, hipEventRecord(c->hist_ev, s));  // k_count reads them too
+      hist_dirty = 0;
     }
     if (gev && !decide) HIP_TRY(c, hipEventRecord(gev[2], s));
-    if (cloud_mode >= 0 && !fusedfn) {
+    if (cloud_mode >= 0) {
       p.mode = cloud_mode;
       p.cloud_gx = static_cast<int>(grid.x);
-      // at most one chunk per SIMD: all of a chunk's points in one pass
-      KernelFn fn = pick_cloud(cloud_mode, vec, p.n_chunks <= 4 * static_cast<int64_t>(c->n_cu));
+      KernelFn fn = pick_cloud(cloud_mode, vec);
       c->last.p[2] = p;  // (sl_time_kernels re-runs it without the pre-stats workgroups)
       c->last.fn[2] = reinterpret_cast<const void*>(fn);
       Params pc = p;
       dim3 cgrid = grid;
       const bool last_g = g == n_groups - 1;
-      const bool pre_now = pre_run && !pre_dec && last_g;
+      const bool pre_now = pre_run && last_g;
       const bool pre_grp = pre_groups && !last_g;
-      if (pre_now) {  // + the declared next call's histogram pass, after this group's triangulating workgroups
-        r = add_pre(pc, cgrid, nv, c->decl_stack, c->decl_vs, std::min(vpg, c->decl_views));
-        if (r) return r;
-      } else if (pre_grp) {  // + this call's next launch group's
-        r = add_pre(pc, cgrid, nv, p0.stack + static_cast<int64_t>(v0 + vpg) * p0.stack_vs, p0.stack_vs,
-                    std::min(vpg, p0.n_views - v0 - vpg));
-        if (r) return r;
-      }
+      if (pre_now)  // + the declared next call's histogram pass, after this group's triangulating workgroups
+        add_pre(pc, cgrid, nv, c->decl_stack, c->decl_vs, std::min(vpg, c->decl_views));
+      else if (pre_grp)  // + this call's next launch group's
+        add_pre(pc, cgrid, nv, p0.stack + static_cast<int64_t>(v0 + vpg) * p0.stack_vs, p0.stack_vs,
+                std::min(vpg, p0.n_views - v0 - vpg));
       void* args[] = {&pc};
       HIP_TRY(c, hipLaunchKernel(reinterpret_cast<const void*>(fn), cgrid, dim3(kThreads), args, 0, s));
-      if (pre_now) c->pre_armed = true;
-      if (pre_grp) {
-        next_pre = true;
-        pre_in = c->pre_buf;
+      c->super_dirty = false;
+      if (pre_now) {
+        c->pre_armed = true;
+        c->pre_stack = c->decl_stack;
+        c->pre_vs = c->decl_vs;
+        c->pre_views = std::min(vpg, c->decl_views);
+        c->pre_hw = p0.HW;
+        c->pre_capture = cap_id;
       }
+      next_pre = pre_grp;
     }
     if (gev) HIP_TRY(c, hipEventRecord(gev[3], s));
   }
@@ -3403,6 +2670,19 @@ int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mod
   }
   c->last_launches = g;
   return SL_OK;
+}
+
+// launch_groups, and what a failure in it leaves: scratch that may be dirty
+// (cleared before the next call uses it) and no queued pass.
+int launch(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mode, int cloud_mode, hipStream_t s,
+           PreArms arms) {
+  const int r = launch_groups(c, p0, vec, decode_mode, count_mode, cloud_mode, s, arms);
+  if (r) {
+    c->hist_dirty[0] = c->hist_dirty[1] = c->cap_hist;
+    c->super_dirty = c->d_super != nullptr;
+    c->pre_armed = false;
+  }
+  return r;
 }
 
 // The context's scratch is shared by its calls: a call on another stream than
@@ -3550,33 +2830,16 @@ int sl_ctx_create(int device, sl_ctx** out) {
     delete c;
     return SL_EHIP;
   }
-  // k_decode workgroups per CU when its grid is capped (SLGPU_DECODE_PER_CU,
-  // default kDecodePerCu; 0 = uncapped)
-  int per_cu = kDecodePerCu, n_cu = 0;
-  if (const char* d = getenv("SLGPU_DECODE_PER_CU")) per_cu = atoi(d);
+  // k_decode's grid cap and the pre-stats grid, per CU
+  int n_cu = 0;
   if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < 1)
     n_cu = 256;
   c->n_cu = n_cu;
-  if (per_cu > 0) c->decode_wgs = per_cu * n_cu;
-  if (const char* d = getenv("SLGPU_PATH")) c->force_3k = atoi(d) == 3;
-  if (const char* d = getenv("SLGPU_RECORDS")) c->rec_from_maps = atoi(d) == 0;
-  if (const char* d = getenv("SLGPU_REC12")) c->rec12 = atoi(d) != 0;
+  c->decode_wgs = kDecodePerCu * n_cu;
+  c->pre_wgs = 8 * n_cu;
+  // (test switch: the exact f32 mode through the reference's own operation
+  // sequence instead of the verified route, which the GPU tests compare)
   if (const char* d = getenv("SLGPU_VERIFY32")) c->verify32 = atoi(d) != 0;
-  if (const char* d = getenv("SLGPU_STATS_SIDE")) {
-    c->no_side = atoi(d) == 0;
-    c->side_groups = atoi(d) == 1;
-  }
-  if (const char* d = getenv("SLGPU_XY_CALC")) c->xy_calc_env = atoi(d) != 0;
-  if (const char* d = getenv("SLGPU_FUSED")) c->fused = atoi(d) != 0;
-  if (const char* d = getenv("SLGPU_PRESTATS")) c->no_pre = atoi(d) == 0;
-  if (const char* d = getenv("SLGPU_PRE_GROUPS")) c->no_pre_groups = atoi(d) == 0;
-  if (const char* d = getenv("SLGPU_PRE_MIX")) c->pre_mix = atoi(d);
-  if (const char* d = getenv("SLGPU_PRE_WGS")) c->pre_wgs = std::max(0, atoi(d));
-  if (const char* d = getenv("SLGPU_PRE_DECODE")) c->pre_decode = atoi(d) != 0;
-  if (const char* d = getenv("SLGPU_DECODE_BALANCE")) c->decode_balance = atoi(d) != 0;
-  if (const char* d = getenv("SLGPU_DECODE_DYN")) c->decode_dyn = atoi(d) != 0 ? 1 : 0;
-  if (const char* d = getenv("SLGPU_GROUP_CHUNKS"))
-    c->max_chunks = std::max<int64_t>(1, std::min<int64_t>(kMaxChunks, atoll(d)));
   if (hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return SL_EHIP;
@@ -3593,21 +2856,13 @@ void sl_ctx_destroy(sl_ctx* c) {
   }
   if (c->d_gcounts) (void)hipFree(c->d_gcounts);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
-  if (c->side) {
-    (void)hipStreamSynchronize(c->side);
-    (void)hipStreamDestroy(c->side);
-  }
-  for (hipEvent_t e : {c->hist_ev, c->stats_ev, c->entry_ev})
-    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (void* ptr : {static_cast<void*>(c->d_planes), static_cast<void*>(c->d_xn), static_cast<void*>(c->d_yn),
                     static_cast<void*>(c->d_nc), static_cast<void*>(c->d_stats), static_cast<void*>(c->d_f32),
                     static_cast<void*>(c->d_codes), static_cast<void*>(c->d_hist[0]),
                     static_cast<void*>(c->d_hist[1]), static_cast<void*>(c->d_ptnib),
                     static_cast<void*>(c->d_block_sums), static_cast<void*>(c->d_chunk_counts),
-                    static_cast<void*>(c->d_super[0]), static_cast<void*>(c->d_super[1]),
-                    static_cast<void*>(c->d_lb), static_cast<void*>(c->d_pre[0]),
-                    static_cast<void*>(c->d_pre[1]), static_cast<void*>(c->d_pre[2])})
+                    static_cast<void*>(c->d_super)})
     if (ptr) (void)hipFree(ptr);
   delete c;
 }
@@ -3617,8 +2872,10 @@ const char* sl_ctx_last_error(const sl_ctx* c) { return c ? c->err.c_str() : "nu
 int sl_ctx_reserve(sl_ctx* c, int64_t max_views, int64_t max_px) {
   if (!c || max_views < 1 || max_px < 1) return fail(c, SL_EINVAL, "sl_ctx_reserve: bad sizes");
   HIP_TRY(c, hipSetDevice(c->device));
-  const int64_t vpg = std::max<int64_t>(1, c->max_chunks / ((max_px + kChunk - 1) / kChunk));
-  int r = ensure_scratch(c, std::min(vpg, max_views), max_px, true);
+  // (the histograms for a whole launch group: a pre-stats pass of the next
+  // group or call never needs more)
+  const int64_t vpg = std::max<int64_t>(1, kMaxChunks / ((max_px + kChunk - 1) / kChunk));
+  int r = ensure_scratch(c, std::min(vpg, max_views), max_px, true, vpg);
   if (r) return r;
   return grow(c, &c->d_stats, &c->cap_stats, max_views);
 }
@@ -3675,12 +2932,8 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
   HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&c->d_yn), sizeof(double) * H));
   HIP_TRY(c, hipMemcpy(c->d_yn, yn.data(), sizeof(double) * H, hipMemcpyHostToDevice));
   {
-    // planes32 [Wp][4] | xn32 [W] | yn32 [H] | pad to 16 B | planes12 [Wp][3] | 1 KB + 16 B of slack
-    const size_t off12 = (4 * static_cast<size_t>(Wp) + W + H + 3) / 4 * 4;
-    std::vector<float> f(off12 + 3 * static_cast<size_t>(Wp) + 260, 0.0f);
-    for (int i = 0; i < Wp; ++i)
-      for (int k = 0; k < 3; ++k) f[off12 + 3 * i + k] = static_cast<float>(pl[4 * i + k]);
-    c->off12 = off12;
+    // planes32 [Wp][4] | xn32 [W] | yn32 [H] | 1 KB of slack
+    std::vector<float> f(4 * static_cast<size_t>(Wp) + W + H + 256, 0.0f);
     for (int i = 0; i < 4 * Wp; ++i) f[i] = static_cast<float>(pl[i]);  // w: f32 of n.Oc + d
     for (int u = 0; u < W; ++u) f[4 * Wp + u] = static_cast<float>(xn[u]);
     for (int v = 0; v < H; ++v) f[4 * Wp + W + v] = static_cast<float>(yn[v]);
@@ -3726,7 +2979,7 @@ int sl_set_calib(sl_ctx* c, int H, int W, const double* K, const double* Oc, con
   c->cam[2] = fx;
   c->cam[3] = fy;
   c->xy_calc = false;
-  if (c->xy_calc_env) {  // may k_cloud compute the rays' x / y?  Checked on the device, entry by entry
+  {  // may k_cloud compute the rays' x / y?  Checked on the device, entry by entry
     int* d_bad = nullptr;
     HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(&d_bad), sizeof(int)));
     int bad = 0;
@@ -3801,7 +3054,6 @@ static void fill_common(sl_ctx* c, Params& p, int n_views, int H, int W) {
   p.planes32 = reinterpret_cast<const float4*>(c->d_f32);
   p.xn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp : nullptr;
   p.yn32 = c->d_f32 ? c->d_f32 + 4 * c->Wp + c->W : nullptr;
-  p.planes12 = c->d_f32 ? c->d_f32 + c->off12 : nullptr;
   p.fast_thr = c->fast_thr;
   p.xy_safe = c->xy_safe ? 1 : 0;
   p.xy_calc = c->xy_calc ? 1 : 0;
@@ -3825,8 +3077,7 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   if (!c) return SL_EINVAL;
   int64_t* masked = c->mc_next;  // armed by sl_mask_counts_to for this call only (consumed even on failure)
   c->mc_next = nullptr;
-  const bool ready = c->ready_next;  // armed by sl_stack_ready for this call only (likewise)
-  const hipEvent_t ready_ev = c->ready_ev_next;
+  const hipEvent_t ready_ev = c->ready_next ? c->ready_ev_next : nullptr;  // sl_stack_ready: this call only (likewise)
   c->ready_next = false;
   c->ready_ev_next = nullptr;
   const PreArms arms = take_arms(c);  // sl_stack_next's declaration, a queued pre-stats pass (likewise)
@@ -3889,14 +3140,14 @@ int sl_decode_triangulate(sl_ctx* c, const uint8_t* stack, int64_t stack_vs, int
   // k_decode ([k_stats] + k_decode + k_cloud), else k_decode + k_count + k_cloud
   // (a maps-only call reads no calibration table: k_decode loads its tables
   // only for a cloud, whose calibration common_out_checks matched to H x W)
-  const bool decide = vec && !c->force_3k && W <= kDecX && H <= kDecY &&
+  const bool decide = vec && W <= kDecX && H <= kDecY &&
                       (!xyz || (c->has_calib && c->W == W && c->H == H && c->Wp <= kDecPl));
   HIP_TRY(c, hipSetDevice(c->device));
   const hipStream_t s = static_cast<hipStream_t>(stream);
   r = stream_handoff(c, s);
   if (r) return r;
-  return launch(c, p, vec, decide ? (decode_mode | M_DECIDE) : decode_mode, count_mode, cloud_mode, s, arms,
-                ready, ready_ev);
+  if (ready_ev) HIP_TRY(c, hipStreamWaitEvent(s, ready_ev, 0));  // the caller's promise, kept on the stream
+  return launch(c, p, vec, decide ? (decode_mode | M_DECIDE) : decode_mode, count_mode, cloud_mode, s, arms);
 }
 
 int sl_stack_ready(sl_ctx* c, void* event) {
@@ -4063,34 +3314,53 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
   if (!c->last.valid) return fail(c, SL_EINVAL, "sl_time_kernels: no earlier call to re-run");
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->last.s;
-  hipEvent_t ev[4];
-  for (int k = 0; k < 4; ++k) HIP_TRY(c, hipEventCreate(&ev[k]));
-  int r = SL_OK;
-  // k_cloud, then k_count, then k_decode: the consumers first -- k_cloud reads
-  // the block and super-block sums (which the producers' re-runs add into
-  // again) and k_decode's records; k_count reads the histogram k_decode's
-  // re-runs accumulate into (reset below)
-  // (M_DECIDE: k_cloud, then k_decode -- it reads the histograms k_stats'
-  // re-runs accumulate into -- then k_stats)
-  // k_cloud re-runs first in both paths: the producers' re-runs (k_count /
-  // k_decode) add their block sums into the super-block sums again
+  // The launch consumed its inputs (its k_decode / k_count zeroed the
+  // histograms they read, its k_cloud the super-block sums): from clean
+  // scratch they are rebuilt once, untimed, then every kernel re-runs with
+  // `rerun` set (consumers leave their inputs as they are).  k_cloud first --
+  // it reads the super-block sums the producers' re-runs add into again --
+  // then k_decode (M_DECIDE; k_count otherwise), which reads the histograms
+  // that k_stats' (k_decode's) re-runs accumulate into, then k_stats (k_decode).
+  // Afterwards the scratch is cleared again: a pass queued for the next call
+  // is dropped (that call computes its own histograms).
+  Params pr[3];
+  for (int k = 0; k < 3; ++k) {
+    pr[k] = c->last.p[k];
+    pr[k].rerun = 1;
+  }
+  auto run = [&](const void* fn, int k) -> hipError_t {
+    Params q = pr[k];
+    void* args[] = {&q};
+    return hipLaunchKernel(fn, c->last.grid[k], dim3(kThreads), args, 0, s);
+  };
+  auto clear = [&]() -> hipError_t {
+    hipError_t e = hipMemsetAsync(c->d_hist[0], 0, sizeof(unsigned) * c->cap_hist, s);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_hist[1], 0, sizeof(unsigned) * c->cap_hist, s);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_super, 0, sizeof(unsigned) * kSuperWords, s);
+    return e;
+  };
+  hipError_t e = clear();
+  if (e == hipSuccess && c->last.decide && c->last.stats) e = run(reinterpret_cast<const void*>(k_stats), 1);
+  if (e == hipSuccess) e = run(c->last.fn[0], 0);
+  if (e == hipSuccess && !c->last.decide && c->last.fn[1]) e = run(c->last.fn[1], 1);
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int k = 0; k < 4 && e == hipSuccess; ++k) e = hipEventCreate(&ev[k]);
+  int r = e == hipSuccess ? SL_OK : fail(c, SL_EHIP, std::string("sl_time_kernels: ") + hipGetErrorString(e));
   const int order3[3] = {2, 1, 0}, orderd[3] = {2, 0, 1};
   const int* order = c->last.decide ? orderd : order3;
-  HIP_TRY(c, hipEventRecord(ev[0], s));
+  if (r == SL_OK && hipEventRecord(ev[0], s) != hipSuccess) r = fail(c, SL_EHIP, "hipEventRecord");
   for (int q = 0; q < 3 && r == SL_OK; ++q) {
     const int k = order[q];
     if (c->last.fn[k]) {
-      Params p = c->last.p[k];
-      void* args[] = {&p};
       for (int i = 0; i < reps; ++i) {
-        const hipError_t e = hipLaunchKernel(c->last.fn[k], c->last.grid[k], dim3(kThreads), args, 0, s);
+        e = run(c->last.fn[k], k);
         if (e != hipSuccess) {
           r = fail(c, SL_EHIP, std::string("sl_time_kernels: ") + hipGetErrorString(e));
           break;
         }
       }
     }
-    if (hipEventRecord(ev[q + 1], s) != hipSuccess && r == SL_OK) r = fail(c, SL_EHIP, "hipEventRecord");
+    if (r == SL_OK && hipEventRecord(ev[q + 1], s) != hipSuccess) r = fail(c, SL_EHIP, "hipEventRecord");
   }
   double out[3] = {0.0, 0.0, 0.0};
   if (r == SL_OK && hipEventSynchronize(ev[3]) == hipSuccess) {
@@ -4104,17 +3374,14 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
   // that its launch leaves exhausted: each re-run gets fresh counters (zeroed
   // outside its events) and is timed alone
   if (r == SL_OK && c->last.fn[0] && c->last.p[0].decode_dyn) {
-    Params p = c->last.p[0];
-    void* args[] = {&p};
     const unsigned nv = c->last.grid[0].y;
-    unsigned* ctr = p.super_sums + (p.super_cap - nv);
+    unsigned* ctr = c->d_super + (kSuperCap - nv);  // (buffer 0: the re-runs leave the selectors at 0)
     double sum = 0.0;
     for (int i = 0; i < reps && r == SL_OK; ++i) {
       float ms = 0.f;
       if (hipMemsetAsync(ctr, 0, sizeof(unsigned) * nv, s) != hipSuccess || hipEventRecord(ev[0], s) != hipSuccess ||
-          hipLaunchKernel(c->last.fn[0], c->last.grid[0], dim3(kThreads), args, 0, s) != hipSuccess ||
-          hipEventRecord(ev[1], s) != hipSuccess || hipEventSynchronize(ev[1]) != hipSuccess ||
-          hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess) {
+          run(c->last.fn[0], 0) != hipSuccess || hipEventRecord(ev[1], s) != hipSuccess ||
+          hipEventSynchronize(ev[1]) != hipSuccess || hipEventElapsedTime(&ms, ev[0], ev[1]) != hipSuccess) {
         r = fail(c, SL_EHIP, "sl_time_kernels: dynamic k_decode re-run");
         break;
       }
@@ -4122,9 +3389,13 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
     }
     if (r == SL_OK) out[0] = sum / reps;
   }
-  for (int k = 0; k < 4; ++k) (void)hipEventDestroy(ev[k]);
-  // the re-runs accumulated into the histograms: the next calls start from zero
-  for (int b = 0; b < 2; ++b) c->hist_dirty[b] = c->cap_hist[b];
+  for (int k = 0; k < 4; ++k)
+    if (ev[k]) (void)hipEventDestroy(ev[k]);
+  // the re-runs accumulated into the histograms and the super-block sums
+  if (clear() != hipSuccess && r == SL_OK) r = fail(c, SL_EHIP, "sl_time_kernels: scratch reset");
+  c->hist_dirty[0] = c->hist_dirty[1] = 0;
+  c->super_dirty = r != SL_OK;
+  c->pre_armed = false;
   c->last.valid = false;
   if (decode_ms) *decode_ms = out[0];
   if (count_ms) *count_ms = out[1];
@@ -4134,7 +3405,7 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
 
 int sl_last_launch_info(sl_ctx* c, int* path, int64_t* launches, int64_t* last_launch_px) {
   if (!c) return SL_EINVAL;
-  if (path) *path = c->last.fused ? 2 : c->last.decide ? 1 : 0;
+  if (path) *path = c->last.decide ? 1 : 0;
   if (launches) *launches = c->last_launches;
   if (last_launch_px) *last_launch_px = c->last_launch_px;
   return SL_OK;

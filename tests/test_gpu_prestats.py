@@ -34,7 +34,7 @@ def test_chained_calls_bit_identical():
     the histograms computed by the previous call's k_cloud; a declaration that
     does not match the next call (another buffer) is ignored; a fixed-mask call
     in the chain consumes nothing but still queues the pass for its successor;
-    three rounds go through the three-buffer rotation more than once."""
+    three rounds of it."""
     from structured_light_for_3d_model_replication_amd import core, synth
     H, W = 480, 640
     rig = synth.Rig(H=H, W=W)
@@ -68,18 +68,10 @@ def test_chained_calls_bit_identical():
     np.testing.assert_array_equal(ref[1][0], P.astype(np.float32))
 
 
-@pytest.mark.parametrize("env", [{}, {"SLGPU_PRE_MIX": "1"}, {"SLGPU_PRE_WGS": "7"},
-                                 {"SLGPU_PRE_MIX": "1", "SLGPU_PRE_WGS": "600"}, {"SLGPU_PRE_DECODE": "1"},
-                                 {"SLGPU_PRE_DECODE": "1", "SLGPU_PRE_WGS": "5"}])
-def test_chained_calls_without_syncs(env, monkeypatch):
+def test_chained_calls_without_syncs():
     """The same chain queued back to back (no host sync between calls, each
     call into its own outputs): the pass a call's k_cloud runs and the next
-    call's decode are ordered by the stream alone.  Also with the pre-stats
-    workgroups spread among the triangulating ones, and with fewer / more of
-    them than k_stats' grid, and with them in k_decode's tail instead (A/B
-    switches, read at context creation)."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    call's decode are ordered by the stream alone."""
     from structured_light_for_3d_model_replication_amd import core, synth
     H, W = 240, 320
     rig = synth.Rig(H=H, W=W)
@@ -137,9 +129,10 @@ def test_chained_multi_group_calls():
 
 
 def test_chain_survives_kernel_reruns():
-    """sl_time_kernels between chained calls (it re-runs the last group's
-    kernels, the pre-stats workgroups left out): the next call still takes
-    intact histograms."""
+    """sl_time_kernels between chained calls (it rebuilds the inputs the call
+    consumed, re-runs the last group's kernels without the pre-stats
+    workgroups and drops the queued pass): the next call computes its own
+    histograms, bit-identical results."""
     from structured_light_for_3d_model_replication_amd import core, synth
     H, W = 480, 640
     rig = synth.Rig(H=H, W=W)
@@ -263,13 +256,12 @@ def _group_views(H, W, V, maps, seed0):
 
 
 @pytest.mark.parametrize("maps", [False, True])
-def test_multi_group_call_prestats_between_groups(maps, monkeypatch):
+def test_multi_group_call_prestats_between_groups(maps):
     """One call of three launch groups (70 1080p views: 32 + 32 + 6): groups 2
     and 3 take the histograms the previous group's k_cloud computed (no k_stats
     launch).  Every view's thresholds, cloud slice (and maps) equal those of
-    the same view decoded alone; the whole output equals a context with the
-    pass between groups switched off (SLGPU_PRE_GROUPS=0, A/B); one view of the
-    last group against the oracle."""
+    the same view decoded alone; one view of the last group against the
+    oracle."""
     from structured_light_for_3d_model_replication_amd import core, synth
     H, W, V = 1080, 1920, 70
     rig, base, A, TA = _group_views(H, W, V, maps, 300)
@@ -297,12 +289,6 @@ def test_multi_group_call_prestats_between_groups(maps, monkeypatch):
                 np.testing.assert_array_equal(got[k][v], ref[k][0], err_msg=f"view {v} map {k}")
         np.testing.assert_array_equal(np.array(eng.last_thresholds(v), dtype=np.float64), ref[-1],
                                       err_msg=f"view {v} thresholds")
-    monkeypatch.setenv("SLGPU_PRE_GROUPS", "0")
-    eng0 = core.Reconstructor(torch.device("cuda", 0))
-    eng0.set_calibration(cal, H, W)
-    r0 = eng0.decode_triangulate(A, out={}, **kw)
-    eng0.sync()
-    _same(got, _snap(r0, eng0)[:-1], "SLGPU_PRE_GROUPS=0")
     v = 67  # last group
     col, row, mask, P, C = o.decode_triangulate(list(A[v].cpu().numpy()), TA[v].cpu().numpy(), cal)
     np.testing.assert_array_equal(got[0][off[v]:off[v + 1]], P.astype(np.float32))
@@ -389,34 +375,144 @@ def test_prepared_call_after_close_raises():
         pc.run()
 
 
-@pytest.mark.parametrize("maps", [False, True])
-def test_decode_dynamic_groups_identical(maps, monkeypatch):
-    """The dynamic decode grid (k_decode's chunk groups after the first round
-    pulled from per-view counters; the default for cloud-only calls,
-    SLGPU_DECODE_DYN=1 forces it on maps calls too): outputs identical to the
-    strided grid (SLGPU_DECODE_DYN=0), on 1080p views whose chunk groups
-    outnumber the capped grid, chained (pre-stats) and not."""
+def test_decode_dynamic_grid_equals_strided():
+    """The dynamic decode grid (cloud-only calls: k_decode's chunk groups after
+    the first round pulled from per-view counters in the super-block buffer,
+    which k_cloud zeroes) against the strided grid of a maps call: identical
+    clouds, chained (pre-stats) and not, on 1080p views whose chunk groups
+    outnumber the capped grid; sl_time_kernels re-runs the dynamic k_decode on
+    fresh counters (a full decode each time)."""
     from structured_light_for_3d_model_replication_amd import core, synth
     H, W, V = 1080, 1920, 3
-    rig, base, A, TA = _group_views(H, W, V, maps, 500)
+    rig, base, A, TA = _group_views(H, W, V, True, 500)
     cal = synth.make_calibration(rig, with_Nc=False)
-    kw = dict(texture=TA, maps=maps, cloud=True, xyz_dtype=torch.float32)
-    monkeypatch.setenv("SLGPU_DECODE_DYN", "0")
     eng = core.Reconstructor(torch.device("cuda", 0))
     eng.set_calibration(cal, H, W)
-    ref = _snap(eng.decode_triangulate(A, out={}, **kw), eng)[:-1]
+    ref = _snap(eng.decode_triangulate(A, out={}, texture=TA, maps=True, cloud=True, xyz_dtype=torch.float32),
+                eng)[:3]
     eng.sync()
-    monkeypatch.setenv("SLGPU_DECODE_DYN", "1")
-    dyn = core.Reconstructor(torch.device("cuda", 0))
-    dyn.set_calibration(cal, H, W)
-    for k in range(3):
-        r = dyn.decode_triangulate(A, out={}, next_stack=A if k < 2 else None, **kw)
-        dyn.sync()
-        _same(_snap(r, dyn)[:-1], ref, f"dynamic call {k}")
-    # sl_time_kernels re-runs the dynamic k_decode on fresh counters: a full
-    # decode each time (an exhausted counter would leave a near-empty launch)
-    eng.decode_triangulate(A, out={}, **kw)
     t_ref = eng.time_kernels(5)
-    dyn.decode_triangulate(A, out={}, **kw)
-    t_dyn = dyn.time_kernels(5)
-    assert t_dyn[0] > 0.6 * t_ref[0], (t_dyn, t_ref)
+    for k in range(3):
+        r = eng.decode_triangulate(A, out={}, texture=TA, maps=False, cloud=True, xyz_dtype=torch.float32,
+                                   next_stack=A if k < 2 else None)
+        eng.sync()
+        _same(_snap(r, eng)[:3], ref, f"dynamic call {k}")
+    t_dyn = eng.time_kernels(5)
+    assert t_dyn[0] > 0.3 * t_ref[0], (t_dyn, t_ref)
+    r = eng.decode_triangulate(A, out={}, texture=TA, maps=False, cloud=True, xyz_dtype=torch.float32)
+    eng.sync()
+    _same(_snap(r, eng)[:3], ref, "after the re-runs")
+
+
+def test_graphs_replay_in_any_phase():
+    """Phase safety: graphs of 1, 3 and 5 chained
+    calls over three views (odd launch-group counts, their last call queuing a
+    pass for a stack the graph's first call does not decode), each replayed
+    several times, interleaved with one another, with eager chained calls
+    (whose queued pass a replay must not disturb) and with sl_time_kernels:
+    every call's maps, mask, thresholds and cloud bit-identical to the same
+    call made alone, and one view to the oracle."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W = 480, 640
+    rig = synth.Rig(H=H, W=W)
+    cal = synth.make_calibration(rig)
+    views = [synth.render_stack(rig, seed=140 + v, view_deg=30.0 * v, device="cuda") for v in range(3)]
+    views[2][0][1].add_(25)  # a brighter black plane: other thresholds
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    kw = dict(maps=True, cloud=True, xyz_dtype=torch.float32)
+    ref = []
+    for st, tx in views:
+        ref.append(_snap(eng.decode_triangulate(st, texture=tx, out={}, **kw), eng))
+        eng.sync()
+    assert not np.array_equal(ref[0][-1], ref[2][-1])
+    s = torch.cuda.Stream()
+
+    def call(i, o, nxt):
+        st, tx = views[i]
+        return eng.decode_triangulate(st, texture=tx, out=o, next_stack=views[nxt][0], **kw)
+
+    graphs = {}
+    for K in (1, 3, 5):
+        seq = [(k + K) % 3 for k in range(K)]
+        nxt = [(i + 1) % 3 for i in seq]  # the last call names a stack the first does not decode (K = 3 aside)
+        outs = [{} for _ in range(K)]
+        with torch.cuda.stream(s):
+            for k in range(K):  # eager first: the outputs are allocated outside the capture
+                call(seq[k], outs[k], nxt[k])
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+            res = [call(seq[k], outs[k], nxt[k]) for k in range(K)]
+        graphs[K] = (g, seq, res, outs)
+
+    def replay(K, what):
+        g, seq, res, outs = graphs[K]
+        for o_ in outs:
+            for v in o_.values():
+                v.zero_()
+        with torch.cuda.stream(s):
+            g.replay()
+        torch.cuda.synchronize()
+        for k, r in enumerate(res):
+            _same(_snap(r, eng)[:-1], ref[seq[k]][:-1], f"{what}: graph {K}, call {k}")
+
+    def eager(i, nxt, what):
+        with torch.cuda.stream(s):
+            r = call(i, {}, nxt)
+        torch.cuda.synchronize()
+        _same(_snap(r, eng), ref[i], what)
+
+    replay(5, "first replay")
+    replay(1, "first replay")
+    replay(1, "again")
+    eager(0, 1, "eager 0 (queues a pass for 1)")
+    replay(3, "between eager calls")
+    replay(5, "between eager calls")
+    eager(1, 2, "eager 1 takes its pass after two replays")
+    replay(3, "again")
+    eng.time_kernels(2)
+    replay(5, "after re-runs")
+    eager(2, 0, "eager after a replay")
+    replay(1, "last")
+    st, tx = views[2]
+    col, row, mask, P, C = o.decode_triangulate(list(st.cpu().numpy()), tx.cpu().numpy(), cal)
+    np.testing.assert_array_equal(ref[2][3][0], col)
+    np.testing.assert_array_equal(ref[2][5][0], mask)
+    np.testing.assert_array_equal(ref[2][0], P.astype(np.float32))
+
+
+def test_reserve_then_capture_multi_group_call():
+    """reserve() sizes every scratch buffer a captured call needs --
+    the histograms of a whole launch group included -- so a call of two launch
+    groups (34 1080p views: 32 + 2, the pass between its groups) captured right
+    after reserve(), with no eager call first, allocates nothing and replays
+    (twice) to the clouds of the same call made eagerly on another context."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    H, W, V = 1080, 1920, 34
+    rig, base, A, TA = _group_views(H, W, V, False, 620)
+    cal = synth.make_calibration(rig, with_Nc=False)
+    kw = dict(texture=TA, maps=False, cloud=True, xyz_dtype=torch.float32)
+    ref_eng = core.Reconstructor(torch.device("cuda", 0))
+    ref_eng.set_calibration(cal, H, W)
+    ref = _snap(ref_eng.decode_triangulate(A, out={}, **kw), ref_eng)[:3]
+    ref_eng.sync()
+    assert ref_eng.last_launch_info()[1] == 2
+    ref_eng.close()
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(cal, H, W)
+    eng.reserve(V, H * W)
+    out = {"xyz": torch.empty((V * H * W, 3), dtype=torch.float32, device="cuda"),
+           "bgr": torch.empty((V * H * W, 3), dtype=torch.uint8, device="cuda"),
+           "view_offsets": torch.empty(V + 1, dtype=torch.int64, device="cuda")}
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+        r = eng.decode_triangulate(A, out=out, **kw)
+    for rep in range(2):
+        out["xyz"].zero_()
+        with torch.cuda.stream(s):
+            g.replay()
+        torch.cuda.synchronize()
+        _same(_snap(r, eng)[:3], ref, f"replay {rep}")
