@@ -27,7 +27,9 @@ then an identical window with one HIP event per step boundary on the stream
 so they stay out of the headline window).  Max over ranks.
 
 Default workload = BASELINE config 2: one 3840x2160 view, 11+11-bit
-column+row Gray code with inverses (46 planes), per GPU per step.
+column+row Gray code with inverses (46 planes), per GPU per step; the steps
+cycle through three distinct resident views (--ring), so that nothing of a
+view stays in the 256 MB Infinity Cache until its next step.
 Multi-GPU: weak scaling by default (views sharded over ranks with no
 data-path collective); the gather of the clouds to rank 0 (RCCL: torch's
 communicator, or ``--gather native`` = the library's own sl_gather) is timed
@@ -63,7 +65,8 @@ CONFIGS = {
     # c3: the 36-view turntable scan (strong scaling shards it).
     "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0,
                streams=3),  # with next-stats (2 launches per call): 3 lanes best
-    "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0),
+    "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0,
+               ring=3),  # three distinct resident views cycled (no Infinity-Cache carry-over)
     "c3": dict(H=1080, W=1920, Wp=1920, Hp=1080, rows=True, views=36, maps=False, pose=False, deg=10.0,
                streams=2),
     "c4": dict(H=3000, W=4000, Wp=1920, Hp=1080, rows=True, views=45, maps=False, pose=False, deg=1.0,
@@ -133,9 +136,11 @@ def parse(argv=None):
                     help="N > 1: also time BASELINE config 3 strong-scaled (36 views sharded over the N ranks) "
                          "and report it in multi_gpu.strong_c3 (default)")
     ap.add_argument("--no-strong-leg", dest="strong_leg", action="store_false")
-    ap.add_argument("--ring", type=int, default=1,
-                    help="one view in flight (c1 / c2): the headline window cycles through this many distinct "
-                         "resident views (stack, texture and outputs each), chained; 1 = the same view every step")
+    ap.add_argument("--ring", type=int, default=None,
+                    help="one view in flight: the headline window cycles through this many distinct resident "
+                         "views (stack, texture and outputs each), chained; 1 = the same view every step.  Default "
+                         "(CONFIGS): c2 3 -- one view's texture, records and outputs stayed in the 256 MB Infinity "
+                         "Cache from step to step and made the one-view window 3.5 %% faster (DESIGN.md 6.1)"),
     ap.add_argument("--ring-control", dest="ring_control", type=int, default=3,
                     help="one view in flight: a second window with this many distinct views when the headline "
                          "uses one (or one view when the headline cycles several), reported in "
@@ -703,7 +708,7 @@ def main():
     # slot's stack (sl_stack_next)
     ring = {"R": 1, "i": 0}
     slots = [dict(stack=stack, tex=tex, out=out)]
-    ring_R = max(1, a.ring) if pool is None and V == 1 else 1
+    ring_R = max(1, a.ring if a.ring is not None else cfg.get("ring", 1)) if pool is None and V == 1 else 1
     ctl_R = 0
     if pool is None and V == 1 and a.ring_control > 0:
         ctl_R = a.ring_control if ring_R == 1 else 1
@@ -1034,7 +1039,9 @@ def main():
             "config": {"workload": f"BASELINE config {cfg_idx}: {V} x {W}x{H} view(s) per GPU per step ({a.scaling} scaling, {V_total} in all), "
                                    f"{n_planes}-plane stacks (Gray {nc}+{n_planes // 2 - 1 - nc} bits + inverses), "
                                    + ("col/row/mask maps + " if maps else "")
-                                   + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else ""),
+                                   + "fp32 xyz/BGR cloud" + (" with turntable pose" if poses is not None else "")
+                                   + (f"; the steps cycle through {ring_R} distinct resident views (chained)"
+                                      if ring_R > 1 else ""),
                        "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
                        "parallelism": f"views sharded over {world} GPU(s)", "streams_per_gpu": S,
                        "next_stats": bool(a.next_stats)},

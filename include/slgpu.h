@@ -323,7 +323,13 @@ int sl_icp_point_to_plane(sl_ctx* ctx, const double* source, int64_t n_src, cons
  * KDTreeFlann::SearchHybrid(p, radius, max_nn) of every point of xyz [n][3]
  * (device f64): the points with ((dx^2 + dy^2) + dz^2) < radius^2 (itself
  * included) in ascending (d2, index), the first max_nn -> out_idx /
- * out_d2 [n][max_nn] and out_cnt [n] (device).  max_nn <= 1024.  Blocking. */
+ * out_d2 [n][max_nn] and out_cnt [n] (device).  max_nn <= 1024.  Blocking.
+ * Ties (a documented deviation): equal distances are ordered by index here
+ * and in sl_estimate_normals / sl_compute_fpfh; nanoflann leaves them in its
+ * KD-tree traversal order (an unstable sort), so with duplicate points Open3D
+ * may pick another neighbour set or "self" entry.  No reference fixture covers
+ * it; the oracle (oracle/registration_oracle.py) states the same rule, and
+ * parity with Open3D stays unpinned. */
 int sl_radius_search(sl_ctx* ctx, const double* xyz, int64_t n, double radius, int max_nn, int32_t* out_idx,
                      double* out_d2, int32_t* out_cnt, void* stream);
 
@@ -339,9 +345,10 @@ int sl_compute_fpfh(sl_ctx* ctx, const double* xyz, const double* normals, int64
 
 /* The nearest row of b [nb][dim] for every row of a [na][dim] (device f64;
  * dim == 33): nanoflann's L2 order (four dimensions at a time, then the
- * rest), ties to the lower index -> out [na] (device int32); -1 for a row with
- * no distance below +inf (NaN features never match, as nanoflann's strict
- * compare).  Blocking. */
+ * rest), ties to the lower index (a documented deviation: nanoflann's 1-NN
+ * keeps the first candidate its tree traversal meets) -> out [na] (device
+ * int32); -1 for a row with no distance below +inf (NaN features never match,
+ * as nanoflann's strict compare).  Blocking. */
 int sl_feature_nn(sl_ctx* ctx, const double* a, int64_t na, const double* b, int64_t nb, int dim, int32_t* out,
                   void* stream);
 
