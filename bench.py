@@ -148,7 +148,7 @@ def parse(argv=None):
                          "(0: off)")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
-                         "scripts/traffic_from_pmc.py); default profiles/r04_traffic/traffic_<config>.json")
+                         "scripts/traffic_from_pmc.py); default profiles/r05_traffic/traffic_<config>.json")
     return ap.parse_args(argv)
 
 
@@ -1010,12 +1010,12 @@ def main():
         # of the same command, from a committed profile -- not measured here
         traffic = traffic_k = None
         if a.traffic is None:
-            a.traffic = os.path.join(REPO, "profiles", "r04_traffic", f"traffic_{a.config}.json")
+            a.traffic = os.path.join(REPO, "profiles", "r05_traffic", f"traffic_{a.config}.json")
         if os.path.exists(a.traffic):
             try:
                 tj = json.load(open(a.traffic))
                 if tj.get("config") == a.config and tj.get("views") == V and tj.get("decide", False) == decide \
-                        and tj.get("xyz") == ("fast" if head_fast else "exact"):
+                        and tj.get("xyz") == ("fast" if head_fast else "exact") and tj.get("ring", 1) == ring_R:
                     traffic = tj.get("bytes_per_step")
                     traffic_k = tj.get("kernels", {}).get("k_decode")  # per step: all its launches
                     if traffic_k is not None:

@@ -72,6 +72,11 @@ if "--per-step" in args:
     i = args.index("--per-step")
     PER_STEP = int(args[i + 1])
     del args[i:i + 2]
+RING = 1  # --ring R: the steps cycled through R distinct resident views (bench.py --ring)
+if "--ring" in args:
+    i = args.index("--ring")
+    RING = int(args[i + 1])
+    del args[i:i + 2]
 fetch, write = per_kernel(args[0], "FETCH_SIZE"), per_kernel(args[1], "WRITE_SIZE")
 cfg, views, xyz, decide, out = args[2], int(args[3]), args[4], args[5] == "1", args[6]
 kern = {k: (2 * fetch.get(k, 0.0) + write.get(k, 0.0)) * 1024 for k in sorted(set(fetch) | set(write))}
@@ -96,7 +101,7 @@ kern_use = {k: corrected(k) for k in kern} if cal else kern
 for k, v in kern_use.items():
     short[k.split("<")[0]] = short.get(k.split("<")[0], 0.0) + v
 res = {
-    "config": cfg, "views": views, "xyz": xyz, "decide": decide,
+    "config": cfg, "views": views, "xyz": xyz, "decide": decide, "ring": RING,
     "bytes_per_step": sum(kern_use.values()),
     "bytes_per_step_raw": sum(kern.values()),
     "kernels": short,

@@ -104,14 +104,14 @@ def test_bench_defaults_next_stats_and_graph():
 
 
 def test_committed_traffic_profiles_match_the_configs():
-    """bench.py attaches profiles/r04_traffic/traffic_<config>.json to a line
+    """bench.py attaches profiles/r05_traffic/traffic_<config>.json to a line
     only when the profile's workload is the line's (config, views per GPU,
     decide path, exact xyz): every config of the bench but c1 has one that
     matches, with calibrated per-kernel bytes that add up."""
     sys.path.insert(0, REPO)
     import bench
     for name in ("c2", "c3", "c4", "c5"):
-        path = os.path.join(REPO, "profiles", "r04_traffic", f"traffic_{name}.json")
+        path = os.path.join(REPO, "profiles", "r05_traffic", f"traffic_{name}.json")
         tj = json.load(open(path))
         assert tj["config"] == name and tj["views"] == bench.CONFIGS[name]["views"], name
         assert tj["decide"] is True and tj["xyz"] == "exact" and tj["calibration"], name
