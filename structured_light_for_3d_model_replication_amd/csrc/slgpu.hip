@@ -75,6 +75,7 @@ constexpr int kRing = 40;               // stack planes in flight per lane
 // Infinity Cache; cloud-only records leave write-through (sc1, aux 16).
 constexpr int kLoadAux = 2;
 constexpr int kRecAux = 16;
+constexpr int kMapAux = 2;  // nt: the maps and xyz are never read back by the path
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint4 ld_side16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
@@ -978,15 +979,15 @@ __global__ __launch_bounds__(kThreads, 3) void k_decode(Params p) {
           __builtin_amdgcn_wave_barrier();
           const uint4 v = stg[lane];
           __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rd, 1024 * j + 16 * lane, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rd, 1024 * j + 16 * lane, 0, kMapAux);
         }
       }
     } else if (!vec) {
 #pragma unroll
       for (int k = 0; k < kPx; ++k) {
         if (k < n_px) {
-          p.col_out[o + k] = static_cast<int32_t>(col[k]);
-          p.row_out[o + k] = static_cast<int32_t>(row_code(k >> 2, k & 3));
+          __builtin_nontemporal_store(static_cast<int32_t>(col[k]), p.col_out + o + k);
+          __builtin_nontemporal_store(static_cast<int32_t>(row_code(k >> 2, k & 3)), p.row_out + o + k);
         }
       }
     }
@@ -1008,7 +1009,8 @@ __global__ __launch_bounds__(kThreads, 3) void k_decode(Params p) {
       const int mc = wave_sum_dpp(__popc(ok));
       if (lane == 0 && mc) atomicAdd(&s_mcount, static_cast<unsigned>(mc));
     }
-    if ((mode & M_MAPS) && n_px == kPx) *reinterpret_cast<uint4*>(p.mask_out + o) = make_uint4(mb[0], mb[1], mb[2], mb[3]);
+    if ((mode & M_MAPS) && n_px == kPx)
+      __builtin_nontemporal_store(v4u{mb[0], mb[1], mb[2], mb[3]}, reinterpret_cast<v4u*>(p.mask_out + o));
     // ---- |n.r| > 1e-6 (sl_system.py:638-642) of the masked pixels, LDS tables ----
     uint32_t pt = 0u;
     if ((mode & M_CODES) && ok) {
@@ -1323,11 +1325,11 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
     if ((mode & M_MAPS) && (!vec || !codes)) {
       uint8_t* mo_ = p.mask_out + static_cast<int64_t>(view) * HW;
       if (vec) {
-        if (px < HW) *reinterpret_cast<uint32_t*>(mo_ + px) = bytes;
+        if (px < HW) __builtin_nontemporal_store(bytes, reinterpret_cast<uint32_t*>(mo_ + px));
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (px + e < HW) mo_[px + e] = static_cast<uint8_t>((m >> e) & 1u);
+          if (px + e < HW) __builtin_nontemporal_store(static_cast<uint8_t>((m >> e) & 1u), mo_ + px + e);
       }
     }
   }
@@ -1438,7 +1440,7 @@ __device__ __forceinline__ int count_chunk(const Params& p, int64_t gc, int view
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int px = cpx + 256 * s + 4 * lane;
-      if (px < HW) *reinterpret_cast<uint32_t*>(mo_ + px) = mbytes[s];
+      if (px < HW) __builtin_nontemporal_store(mbytes[s], reinterpret_cast<uint32_t*>(mo_ + px));
     }
   }
   total = wave_sum(total);
@@ -1690,6 +1692,11 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
   // assembled by lane permutes into 48 aligned dwords, one store instruction
   // -- and it was slower: c2 124.1-125.4 -> 127.3-127.4 us per step, c5 3.554
   // -> 3.671 ms, same box (profiles/r05_ab/colour_pack_lines.jsonl).)
+  // The xyz leave with nt stores, like k_decode's maps: nothing in the path
+  // reads them back, and default-policy lines would push the records, the
+  // texture and the next view's planes out of L2 / the Infinity Cache (c3-c5
+  // 3-5 % faster per call, c2 3 %; nt colours gained nothing more:
+  // profiles/r05_ab/nt_stores_lines.jsonl).
   for (int j0 = 0; j0 < total; j0 += 64 * kP) {
     if (mode & M_FAST32) {
       // SL_XYZ_F32_FAST (Oc = 0, pinhole rays, no pose; host-checked): the
@@ -1742,9 +1749,9 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         }
         if (j < total) {
           float* xyz = at_bytes(wx, 12u * static_cast<unsigned>(j));
-          xyz[0] = X;
-          xyz[1] = Y;
-          xyz[2] = Z;
+          __builtin_nontemporal_store(X, xyz);
+          __builtin_nontemporal_store(Y, xyz + 1);
+          __builtin_nontemporal_store(Z, xyz + 2);
           uint8_t* cc = at_bytes(wc, 3u * static_cast<unsigned>(j));
           cc[0] = static_cast<uint8_t>(bgr[i]);
           cc[1] = static_cast<uint8_t>(bgr[i] >> 8);
@@ -1989,14 +1996,14 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
         const unsigned o = static_cast<unsigned>(j);  // offset from the chunk's first point
         if (f64out) {
           double* xyz = static_cast<double*>(p.xyz) + 3 * base + 3 * o;
-          xyz[0] = X[i];
-          xyz[1] = Y[i];
-          xyz[2] = Z[i];
+          __builtin_nontemporal_store(X[i], xyz);
+          __builtin_nontemporal_store(Y[i], xyz + 1);
+          __builtin_nontemporal_store(Z[i], xyz + 2);
         } else {
           float* xyz = at_bytes(wx, 12u * o);
-          xyz[0] = static_cast<float>(X[i]);
-          xyz[1] = static_cast<float>(Y[i]);
-          xyz[2] = static_cast<float>(Z[i]);
+          __builtin_nontemporal_store(static_cast<float>(X[i]), xyz);
+          __builtin_nontemporal_store(static_cast<float>(Y[i]), xyz + 1);
+          __builtin_nontemporal_store(static_cast<float>(Z[i]), xyz + 2);
         }
         uint8_t* cc = at_bytes(wc, 3u * o);
         cc[0] = static_cast<uint8_t>(bgr[i]);
