@@ -66,7 +66,8 @@ CONFIGS = {
     "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0,
                streams=3),  # with next-stats (2 launches per call): 3 lanes best
     "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0,
-               ring=3),  # three distinct resident views cycled (no Infinity-Cache carry-over)
+               ring=3, streams=2),  # distinct resident views cycled (no Infinity-Cache
+                                    # carry-over; 3 rounded up to 4, a multiple of the lanes), 2 lanes (5.2)
     "c3": dict(H=1080, W=1920, Wp=1920, Hp=1080, rows=True, views=36, maps=False, pose=False, deg=10.0,
                streams=2),
     "c4": dict(H=3000, W=4000, Wp=1920, Hp=1080, rows=True, views=45, maps=False, pose=False, deg=1.0,
@@ -148,7 +149,7 @@ def parse(argv=None):
                          "(0: off)")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
-                         "scripts/traffic_from_pmc.py); default profiles/r05_traffic/traffic_<config>.json")
+                         "scripts/traffic_from_pmc.py); default profiles/r05_traffic2/traffic_<config>.json")
     return ap.parse_args(argv)
 
 
@@ -693,7 +694,9 @@ def main():
         pool = core.ReconstructorPool(dev, lanes=S, reuse_outputs=True)
         pool.set_calibration(calib, H, W)
         pool.reserve(V, H * W)
-        eng, out = pool.engines[0], pool._outs[0]
+        eng = pool.engines[0]
+        if V > 1:
+            out = pool._outs[0]
 
     # one view in flight: every step on a stream of the bench's own (a graph
     # capture needs a non-default stream, and calls captured on it follow the
@@ -702,34 +705,56 @@ def main():
         torch.cuda.set_stream(torch.cuda.Stream(dev))
     cur = torch.cuda.current_stream(dev)
 
-    # one view in flight: the steps cycle through ring["R"] resident views
-    # (slot 0 = the view above; --ring / --ring-control add distinct ones, each
-    # with its own stack, texture and outputs), every call naming the next
-    # slot's stack (sl_stack_next)
-    ring = {"R": 1, "i": 0}
-    slots = [dict(stack=stack, tex=tex, out=out)]
-    ring_R = max(1, a.ring if a.ring is not None else cfg.get("ring", 1)) if pool is None and V == 1 else 1
-    ctl_R = 0
-    if pool is None and V == 1 and a.ring_control > 0:
-        ctl_R = a.ring_control if ring_R == 1 else 1
-    for k in range(1, max(ring_R, ctl_R)):
-        s_, t_ = synth.render_stack(rig, seed=1000 * cfg_idx + 500 + k, include_rows=rows,
-                                    view_deg=cfg["deg"] * (views[0] + 7 * k), device=dev)
-        slots.append(dict(stack=s_[None].contiguous(), tex=t_[None].contiguous(), out={}))
-        del s_, t_
-    ring["R"] = ring_R
+    # one view per step (V == 1): the steps cycle through the resident views
+    # of ring["slots"] (slot 0 = the view above; --ring / --ring-control add
+    # distinct ones, each with its own stack, texture and outputs), every call
+    # naming its context's next stack (sl_stack_next).  With S lanes, step i
+    # runs on lane i % S and the ring holds a multiple of S views, so a view's
+    # outputs are always written by one lane, in order.
+    ring_req = max(1, a.ring if a.ring is not None else cfg.get("ring", 1)) if V == 1 else 1
+    ctl_req = 0
+    if V == 1 and a.ring_control > 0:
+        ctl_req = 1 if ring_req > 1 else a.ring_control  # the control: one view, or distinct ones
+    slots = [dict(stack=stack, tex=tex, out=out)]  # the distinct resident views
+
+    def ring_of(n):
+        """The slots of a window over n distinct views: n rounded up to a
+        multiple of S; one view: slot 0's stack and texture on every lane, each
+        lane with outputs of its own."""
+        if n <= 1:
+            return [slots[0]] + [dict(stack=stack, tex=tex, out={}) for _ in range(1, S)]
+        while len(slots) < S * -(-n // S):
+            k = len(slots)
+            s_, t_ = synth.render_stack(rig, seed=1000 * cfg_idx + 500 + k, include_rows=rows,
+                                        view_deg=cfg["deg"] * (views[0] + 7 * k), device=dev)
+            slots.append(dict(stack=s_[None].contiguous(), tex=t_[None].contiguous(), out={}))
+            del s_, t_
+        return slots[:S * -(-n // S)]
+
+    head_slots = ring_of(ring_req) if V == 1 else []
+    ctl_slots = ring_of(ctl_req) if ctl_req else []
+    ring_R = len({sl["stack"].data_ptr() for sl in head_slots}) if V == 1 else 1
+    ring = {"slots": head_slots, "i": 0}
 
     def one():
         """One step; -> the stream it ran on."""
-        if pool is None:
-            R = ring["R"]
+        if V == 1:
+            act = ring["slots"]
+            R = len(act)
             i = ring["i"] % R
             ring["i"] += 1
-            sl, nx = slots[i], slots[(i + 1) % R]
-            eng.decode_triangulate(sl["stack"], n_cols, n_rows, texture=sl["tex"], maps=maps, cloud=True,
-                                   xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast, out=sl["out"],
-                                   next_stack=nx["stack"] if a.next_stats else None)
-            return cur
+            sl, nx = act[i], act[(i + S) % R]  # nx: this context's next call
+            if pool is None:
+                eng.decode_triangulate(sl["stack"], n_cols, n_rows, texture=sl["tex"], maps=maps, cloud=True,
+                                       xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast, out=sl["out"],
+                                       next_stack=nx["stack"] if a.next_stats else None)
+                return cur
+            pool._next = i % S
+            res = pool.decode_triangulate(sl["stack"], n_cols, n_rows, texture=sl["tex"], maps=maps, cloud=True,
+                                          xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
+                                          wait_inputs=False, out=sl["out"],
+                                          next_stack=nx["stack"] if a.next_stats else None)
+            return res["stream"]
         res = pool.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
                                       xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
                                       wait_inputs=False,  # resident inputs; outputs never read meanwhile
@@ -743,17 +768,20 @@ def main():
     def sync_all():
         torch.cuda.synchronize(dev)
 
-    for R in sorted({len(slots), ring_R}):  # every slot's outputs allocated before any window
-        ring["R"] = R
-        run_steps(max(a.warmup, S, R))
-    ring["R"] = ring_R
+    for act in ([ctl_slots] if ctl_slots else []) + [head_slots]:  # every slot's outputs allocated before any window
+        ring["slots"], ring["i"] = act, 0
+        run_steps(max(a.warmup, S, len(act)))
     sync_all()
+    if V == 1:
+        out = slots[0]["out"]
     # points per step: the mean over the views the headline cycles through
-    n_pts = sum(int(sl["out"]["view_offsets"][-1].item()) for sl in slots[:ring_R]) / ring_R
+    n_pts = (sum(int(sl["out"]["view_offsets"][-1].item()) for sl in head_slots) / len(head_slots)
+             if V == 1 else int(out["view_offsets"][-1].item()))
 
     def end_on_slot0(k):
         """The next k steps end on slot 0 (whose outputs the verified sample copies)."""
-        ring["i"] = (1 - k) % ring["R"]
+        if V == 1:
+            ring["i"] = (1 - k) % len(ring["slots"])
 
     def timed(k, evs=None):
         """K steps between barrier + synchronize pairs; with ``evs`` (k+1
@@ -764,7 +792,7 @@ def main():
         sync_all()
         t0 = time.perf_counter()
         if evs:
-            evs[0].record(cur if pool is None else pool.streams[pool._next])
+            evs[0].record(cur if pool is None else pool.streams[ring["i"] % S if V == 1 else pool._next])
         for i in range(k):
             st = one()
             if evs:
@@ -859,12 +887,12 @@ def main():
         # Infinity Cache's hits on one view's texture, records and outputs
         # from step to step make the one-view headline faster?
         distinct = None
-        if ctl_R:
-            ring["R"] = ctl_R
+        if ctl_slots:
+            ring["slots"] = ctl_slots
             pre2 = preroll(a.preroll_ms)
             end_on_slot0(a.steps)
             mode2 = "eager"
-            if a.graph:
+            if a.graph and pool is None:
                 try:
                     el_ctl, graph_keep2, _ = timed_graph(a.steps)
                     mode2 = "hipGraph, as the headline"
@@ -878,10 +906,11 @@ def main():
             snap2 = snap_alloc(out, V, maps) if snap is not None else None
             if snap2 is not None:
                 snap_copy(snap2, out, cur)
-            resident = sum(sl["stack"].numel() + sl["tex"].numel() for sl in slots[:ctl_R])
-            distinct = {"views": ctl_R, "ms_per_step": 1e3 * el_ctl / a.steps, "window": mode2,
+            ctl_views = len({sl["stack"].data_ptr() for sl in ctl_slots})
+            resident = sum(sl["stack"].numel() + sl["tex"].numel() for sl in ctl_slots[:ctl_views])
+            distinct = {"views": ctl_views, "ms_per_step": 1e3 * el_ctl / a.steps, "window": mode2,
                         "preroll": pre2, "resident_input_bytes": int(resident), "snap": snap2}
-            ring["R"] = ring_R
+            ring["slots"] = head_slots
     finally:
         gc.enable()
     t = torch.tensor([el_rank], dtype=torch.float64, device=dev)
@@ -1010,7 +1039,7 @@ def main():
         # of the same command, from a committed profile -- not measured here
         traffic = traffic_k = None
         if a.traffic is None:
-            a.traffic = os.path.join(REPO, "profiles", "r05_traffic", f"traffic_{a.config}.json")
+            a.traffic = os.path.join(REPO, "profiles", "r05_traffic2", f"traffic_{a.config}.json")
         if os.path.exists(a.traffic):
             try:
                 tj = json.load(open(a.traffic))

@@ -23,7 +23,7 @@ for spec in "$@"; do
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$cfg -o fetch -- python3 -u scripts/steps_app.py $sel --steps $n > $O/fetch_$cfg.log 2>&1 || { tail -5 $O/fetch_$cfg.log; exit 1; }
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_$cfg -o write -- python3 -u scripts/steps_app.py $sel --steps $n > $O/write_$cfg.log 2>&1 || { tail -5 $O/write_$cfg.log; exit 1; }
   views=$(python3 -c "print({'c2': 1, 'c3': 36, 'c4': 45, 'c5': 45}['$cfg'])")
-  ring=1; [ "$cfg" = c2 ] && ring=3   # steps_app's c2 default: 3 distinct views cycled, as bench.py
+  ring=1; [ "$cfg" = c2 ] && ring=4   # steps_app's c2 default: 3 distinct views rounded up to 4 (2 lanes), as bench.py
   python3 scripts/traffic_from_pmc.py $O/fetch_$cfg $O/write_$cfg $cfg $views exact 1 $O/traffic_$cfg.json --calib $O/cal_f $O/cal_w $O/cal.json --per-step $n --ring $ring > /dev/null || exit 1
   python3 -c "
 import json

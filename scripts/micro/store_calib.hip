@@ -3,9 +3,10 @@
 // under `rocprofv3 --pmc WRITE_SIZE`, so that the PMC write bytes of those
 // kernels can be corrected (MI355X_MICROARCH.md: WRITE_SIZE is exact only for
 // 16-B-per-lane streaming stores).
-//   st16  16 B per lane, 1 KB contiguous per wave instruction (the reference shape)
-//   st12  12 B per lane, 768 B contiguous per wave instruction (k_cloud's xyz,
-//         global_store_dwordx3; k_decode's 12-bit records are 12-B stores too)
+//   st16  16 B per lane, 1 KB contiguous per wave instruction, nontemporal
+//         (k_decode's maps since round 5)
+//   st12  12 B per lane, 768 B contiguous per wave instruction, nontemporal
+//         (k_cloud's xyz, global_store_dwordx3 nt)
 //   st3   3 B per lane (one short + one byte store), 192 B contiguous (k_cloud's BGR)
 //   pts   st12 + st3 interleaved per lane, as k_cloud issues them
 // Each kernel writes kBytes[k] bytes once per launch; 5 launches each.
@@ -21,13 +22,16 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void st16(v4u* o, int64_t n) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
     const unsigned u = static_cast<unsigned>(i);
-    o[i] = v4u{u, u + 1, u + 2, u + 3};
+    __builtin_nontemporal_store(v4u{u, u + 1, u + 2, u + 3}, o + i);
   }
 }
 __global__ __launch_bounds__(256) void st12(F3* o, int64_t n) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
     const float f = static_cast<float>(i);
-    o[i] = F3{f, f + 1.0f, f + 2.0f};
+    float* p = &o[i].x;
+    __builtin_nontemporal_store(f, p);
+    __builtin_nontemporal_store(f + 1.0f, p + 1);
+    __builtin_nontemporal_store(f + 2.0f, p + 2);
   }
 }
 __global__ __launch_bounds__(256) void st3(uint8_t* o, int64_t n) {
@@ -40,7 +44,10 @@ __global__ __launch_bounds__(256) void st3(uint8_t* o, int64_t n) {
 __global__ __launch_bounds__(256) void pts(F3* xyz, uint8_t* bgr, int64_t n) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
     const float f = static_cast<float>(i);
-    xyz[i] = F3{f, f + 1.0f, f + 2.0f};
+    float* p = &xyz[i].x;
+    __builtin_nontemporal_store(f, p);
+    __builtin_nontemporal_store(f + 1.0f, p + 1);
+    __builtin_nontemporal_store(f + 2.0f, p + 2);
     bgr[3 * i] = static_cast<uint8_t>(i);
     bgr[3 * i + 1] = static_cast<uint8_t>(i >> 8);
     bgr[3 * i + 2] = static_cast<uint8_t>(i >> 16);

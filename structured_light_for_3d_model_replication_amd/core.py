@@ -561,7 +561,7 @@ class ReconstructorPool:
         self.streams = [torch.cuda.Stream(self.device) for _ in range(lanes)]
         self._outs = [{} if reuse_outputs else None for _ in range(lanes)]
         self._keys = [None] * lanes  # a lane's last output shapes (reused buffers: no allocation)
-        self._plans = [None] * lanes  # a lane's prepared call and its argument key (resident inputs)
+        self._plans = [{} for _ in range(lanes)]  # a lane's prepared calls by argument key (resident inputs)
         self._next = 0
         self._lock = threading.Lock()
 
@@ -586,7 +586,11 @@ class ReconstructorPool:
         on the caller's stream and the allocator bookkeeping for inputs the
         caller knows are ready and kept alive (e.g. resident stacks).
         ``next_stack``: the stack of THIS LANE's next call (``lanes`` calls
-        later), as Reconstructor.decode_triangulate's."""
+        later), as Reconstructor.decode_triangulate's.  With
+        ``wait_inputs=False`` an explicit ``out`` dict (the caller's buffers
+        for this argument set, e.g. one per resident view) takes the prepared
+        path too; the caller then also guarantees that no other lane writes
+        those buffers meanwhile."""
         if "stream" in kw:
             raise ValueError("ReconstructorPool picks the stream (one per lane)")
         with self._lock:
@@ -598,25 +602,30 @@ class ReconstructorPool:
             for t in (stack, kw.get("texture"), kw.get("poses")):
                 if isinstance(t, torch.Tensor) and t.is_cuda:
                     t.record_stream(st)  # the caller may free it before the lane has read it
-        if not wait_inputs and self._outs[i] is not None and kw.get("out") is None and \
+        outs = kw.get("out") if kw.get("out") is not None else self._outs[i]
+        if not wait_inputs and outs is not None and \
                 kw.get("mask_counts") is None and not kw.get("stack_ready"):
             nxt = kw.pop("next_stack", None)
+            kw.pop("out", None)
             # resident inputs into reused outputs: a prepared call per lane and
             # argument set (sl_call_prepare), re-run with one two-argument call
             tex, pos = kw.get("texture"), kw.get("poses")
             pkey = (stack.data_ptr(), stack.shape, n_cols, n_rows, None if tex is None else tex.data_ptr(),
                     None if pos is None else pos.data_ptr(), kw.get("maps", False), kw.get("cloud", True),
-                    kw.get("xyz_dtype", torch.float32), kw.get("fast_f32", False), kw.get("mask_mode", "adaptive"))
-            plan = self._plans[i]
-            if plan is None or plan[0] != pkey:
+                    kw.get("xyz_dtype", torch.float32), kw.get("fast_f32", False), kw.get("mask_mode", "adaptive"),
+                    id(outs))
+            plans = self._plans[i]
+            ent = plans.get(pkey)  # (the outputs dict, held: its id stays unique) + the prepared call
+            if ent is None:
+                if len(plans) >= 8:  # a bounded set of resident argument sets per lane
+                    for _, q in plans.values():
+                        q.close()
+                    plans.clear()
                 pk = {k: v for k, v in kw.items() if k not in ("mask_counts", "stack_ready")}
                 with torch.cuda.stream(st):  # outputs (re)allocated here belong to the lane stream
-                    pc = eng.prepare(stack, n_cols, n_rows, out=self._outs[i], **pk)
-                if plan is not None:
-                    plan[1].close()
-                plan = self._plans[i] = (pkey, pc)
+                    ent = plans[pkey] = (outs, eng.prepare(stack, n_cols, n_rows, out=outs, **pk))
                 self._keys[i] = None
-            res = dict(plan[1].run(st, next_stack=nxt))
+            res = dict(ent[1].run(st, next_stack=nxt))
             res["stream"] = st
             res["lane"] = i
             return res
@@ -643,9 +652,9 @@ class ReconstructorPool:
             e.sync(st)
 
     def close(self) -> None:
-        for k, plan in enumerate(self._plans):
-            if plan is not None:
-                plan[1].close()
-                self._plans[k] = None
+        for plans in self._plans:
+            for _, pc in plans.values():
+                pc.close()
+            plans.clear()
         for e in self.engines:
             e.close()
