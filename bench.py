@@ -123,9 +123,10 @@ def parse(argv=None):
                          "kernel also computes the next call's adaptive-mask histograms (default)")
     ap.add_argument("--no-next-stats", dest="next_stats", action="store_false")
     ap.add_argument("--graph", dest="graph", action="store_true", default=True,
-                    help="one view in flight: the headline window replays a hipGraph of its K steps, captured "
-                         "(untimed) right after the pre-roll -- every kernel of every step runs, the host enqueues "
-                         "nothing inside the window (default; falls back to eager calls if capture fails)")
+                    help="one lane: the headline window replays a hipGraph of its K steps, captured (untimed) "
+                         "right after the pre-roll -- every kernel of every step runs, the host enqueues nothing "
+                         "inside the window (default; falls back to eager calls if capture fails; with lanes the "
+                         "window is eager: captured lanes measured slower)")
     ap.add_argument("--no-graph", dest="graph", action="store_false")
     ap.add_argument("--verify", dest="verify", action="store_true", default=True,
                     help="after the windows, check the last timed step's outputs of a sample of views (the first "
@@ -698,12 +699,17 @@ def main():
         if V > 1:
             out = pool._outs[0]
 
-    # one view in flight: every step on a stream of the bench's own (a graph
-    # capture needs a non-default stream, and calls captured on it follow the
-    # eager ones with no cross-stream hand-off)
-    if pool is None:
-        torch.cuda.set_stream(torch.cuda.Stream(dev))
+    # a stream of the bench's own (a graph capture needs a non-default
+    # stream): one lane runs every step on it, so calls captured on it follow
+    # the eager ones with no cross-stream hand-off; with lanes it is the
+    # capture's origin, which the lane streams fork from and join
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
     cur = torch.cuda.current_stream(dev)
+
+    def drop_next_all():
+        """sl_stack_next(NULL) on every context (a failed capture's queued passes never ran)."""
+        for e in (pool.engines if pool is not None else [eng]):
+            e.drop_next()
 
     # one view per step (V == 1): the steps cycle through the resident views
     # of ring["slots"] (slot 0 = the view above; --ring / --ring-control add
@@ -736,29 +742,29 @@ def main():
     ring_R = len({sl["stack"].data_ptr() for sl in head_slots}) if V == 1 else 1
     ring = {"slots": head_slots, "i": 0}
 
-    def one():
-        """One step; -> the stream it ran on."""
+    def one(at=None):
+        """One step (the next, or step number ``at``: ring slot at % R, lane
+        at % S); -> the stream it ran on."""
+        if at is None:
+            at = ring["i"]
+            ring["i"] += 1
         if V == 1:
             act = ring["slots"]
-            R = len(act)
-            i = ring["i"] % R
-            ring["i"] += 1
-            sl, nx = act[i], act[(i + S) % R]  # nx: this context's next call
-            if pool is None:
-                eng.decode_triangulate(sl["stack"], n_cols, n_rows, texture=sl["tex"], maps=maps, cloud=True,
-                                       xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast, out=sl["out"],
-                                       next_stack=nx["stack"] if a.next_stats else None)
-                return cur
-            pool._next = i % S
-            res = pool.decode_triangulate(sl["stack"], n_cols, n_rows, texture=sl["tex"], maps=maps, cloud=True,
-                                          xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
-                                          wait_inputs=False, out=sl["out"],
-                                          next_stack=nx["stack"] if a.next_stats else None)
-            return res["stream"]
-        res = pool.decode_triangulate(stack, n_cols, n_rows, texture=tex, maps=maps, cloud=True,
+            sl, nx = act[at % len(act)], act[(at + S) % len(act)]  # nx: this context's next call
+            st_, tx_, o_, nx_ = sl["stack"], sl["tex"], sl["out"], nx["stack"] if a.next_stats else None
+        else:
+            st_, tx_, o_, nx_ = stack, tex, out, nxt
+        if pool is None:
+            eng.decode_triangulate(st_, n_cols, n_rows, texture=tx_, maps=maps, cloud=True,
+                                   xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast, out=o_,
+                                   next_stack=nx_)
+            return cur
+        pool._next = at % S
+        # resident inputs (wait_inputs=False); one view: its own outputs, else
+        # the lane's (never read while the window runs)
+        res = pool.decode_triangulate(st_, n_cols, n_rows, texture=tx_, maps=maps, cloud=True,
                                       xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
-                                      wait_inputs=False,  # resident inputs; outputs never read meanwhile
-                                      next_stack=nxt)
+                                      wait_inputs=False, next_stack=nx_, **({"out": o_} if V == 1 else {}))
         return res["stream"]
 
     def run_steps(k):
@@ -792,7 +798,7 @@ def main():
         sync_all()
         t0 = time.perf_counter()
         if evs:
-            evs[0].record(cur if pool is None else pool.streams[ring["i"] % S if V == 1 else pool._next])
+            evs[0].record(cur if pool is None else pool.streams[ring["i"] % S])
         for i in range(k):
             st = one()
             if evs:
@@ -815,10 +821,11 @@ def main():
     host_enq_ms = [None]
 
     def timed_graph(k):
-        """The headline window as one hipGraph launch: the K steps are captured
-        first (untimed; the library's calls enqueue into the graph exactly as
-        onto the stream, host-side state advancing as for K calls), then the
-        graph is launched once between barrier + synchronize pairs.  -> seconds."""
+        """The headline window as one hipGraph launch (one lane): the K steps
+        are captured first (untimed; the library's calls enqueue into the
+        graph exactly as onto the stream, host-side state advancing as for K
+        calls), then the graph is launched once between barrier + synchronize
+        pairs.  -> (seconds, graph, capture ms)."""
         g = torch.cuda.CUDAGraph()
         t_c = time.perf_counter()
         # thread-local capture: other threads' calls (RCCL's proxy threads) are not disturbed
@@ -864,6 +871,11 @@ def main():
         window = {"mode": "eager: K calls enqueued inside the window"}
         graph_keep = None
         end_on_slot0(a.steps)
+        # with lanes the window is eager: captured, the lanes ran 3-5 % slower
+        # at c2 (one graph forked and joined over the lane streams: 115.2-115.5
+        # vs 109.2-110.1 us; one graph per lane: 118.3-118.6 vs 113.4-114.1 us;
+        # profiles/r05_ab/lanes_graph_lines.jsonl), and the host enqueues the K
+        # prepared calls in ~11 us each, far ahead of the GPU
         if a.graph and pool is None:
             try:
                 el_rank, graph_keep, cap_ms = timed_graph(a.steps)
@@ -873,7 +885,7 @@ def main():
             except Exception as e:  # noqa: BLE001 -- capture unsupported here: the eager window instead
                 window = {"mode": "eager (graph capture failed: %s)" % (str(e)[:160],)}
                 torch.cuda.synchronize(dev)
-                eng.drop_next()  # the captured calls' queued pass never ran
+                drop_next_all()  # the captured calls' queued passes never ran
                 el_rank, _ = timed(a.steps)
         else:
             el_rank, _ = timed(a.steps)
@@ -898,7 +910,7 @@ def main():
                     mode2 = "hipGraph, as the headline"
                 except Exception as e:  # noqa: BLE001
                     torch.cuda.synchronize(dev)
-                    eng.drop_next()
+                    drop_next_all()
                     el_ctl, _ = timed(a.steps)
                     mode2 = "eager (graph capture failed: %s)" % (str(e)[:120],)
             else:
@@ -1119,7 +1131,13 @@ def main():
                                              "overhead); duration: "
                                            + ("HIP events around back-to-back re-runs of the launch "
                                               "(sl_time_kernels)" if rerun_ok
-                                              else "HIP events around the kernel inside the steps")}},
+                                              else "HIP events around the kernel inside the steps"),
+                             "lanes": S,
+                             "lanes_note": None if S == 1 else (
+                                 f"the window keeps {S} calls in flight on {S} streams, and their kernels run "
+                                 "side by side: a rocprofv3 per-dispatch average of this command spans the time a "
+                                 "launch shares the chip with the other lanes' launches (up to "
+                                 f"{S}x this figure); --streams 1 gives the isolated dispatch (DESIGN.md 6.2)")}},
             "path": {"kind": ("k_decode (mask, point decision) + k_cloud (+ the next call's histogram pass: "
                               "sl_stack_next; the first call alone runs k_stats)" if a.next_stats
                               else "k_stats + k_decode (mask, point decision) + k_cloud") if decide
