@@ -759,12 +759,12 @@ def main():
                                    xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast, out=o_,
                                    next_stack=nx_)
             return cur
-        pool._next = at % S
         # resident inputs (wait_inputs=False); one view: its own outputs, else
         # the lane's (never read while the window runs)
         res = pool.decode_triangulate(st_, n_cols, n_rows, texture=tx_, maps=maps, cloud=True,
                                       xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
-                                      wait_inputs=False, next_stack=nx_, **({"out": o_} if V == 1 else {}))
+                                      wait_inputs=False, lane=at % S, next_stack=nx_,
+                                      **({"out": o_} if V == 1 else {}))
         return res["stream"]
 
     def run_steps(k):

@@ -9,6 +9,10 @@
 //   3 the same bytes as 16-B stores (15 B per point: the ideal shape)
 //   4 pattern 0 plus k_cloud's reads (12-bit records 1.5 B/px + texture 3 B/px
 //     of the views' pixels, 16-B loads)
+//   5 pattern 0 with the xyz stores nontemporal (k_cloud since round 5)
+//   6 pattern 3 with nontemporal 16-B stores
+//   7 pattern 0 with the xyz and BGR stores nontemporal
+//   8 pattern 4 with the xyz stores nontemporal (k_cloud's traffic since round 5)
 // One JSON line per pattern: avg / best over 20 timed launches.
 //   cloud_store_floor [views [points_per_view [pixels_per_view]]]
 #include <hip/hip_runtime.h>
@@ -25,25 +29,41 @@ __global__ __launch_bounds__(256) void pts_k(uint8_t* xyz, uint8_t* bgr, const v
   const int64_t nthreads = static_cast<int64_t>(gridDim.x) * 256;
   const int64_t t0 = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   unsigned acc = 0;
-  if (PAT == 4) {  // the read share: nside 16-B words over the grid
+  if (PAT == 4 || PAT == 8) {  // the read share: nside 16-B words over the grid
     for (int64_t g = t0; g < nside; g += nthreads) {
       const v4u r = side[g];
       acc ^= r[0] ^ r[3];
     }
   }
-  if (PAT == 3) {  // 15 B per point as 16-B stores
+  if (PAT == 3 || PAT == 6) {  // 15 B per point as 16-B stores
     const int64_t nw = (15 * npts) / 16;
     for (int64_t i = t0; i < nw; i += nthreads) {
       const unsigned f = static_cast<unsigned>(i);
-      *reinterpret_cast<v4u*>(xyz + 16 * i) = v4u{f, f + 1u, f + 2u, f + 3u};
+      if (PAT == 6) __builtin_nontemporal_store(v4u{f, f + 1u, f + 2u, f + 3u}, reinterpret_cast<v4u*>(xyz + 16 * i));
+      else *reinterpret_cast<v4u*>(xyz + 16 * i) = v4u{f, f + 1u, f + 2u, f + 3u};
     }
   } else {
+    constexpr bool kNtXyz = PAT >= 5, kNtBgr = PAT == 7;
     for (int64_t i = t0; i < npts; i += nthreads) {
       const unsigned f = static_cast<unsigned>(i) ^ acc;
-      if (PAT != 2) *reinterpret_cast<v3u*>(xyz + 12 * i) = v3u{f, f + 1u, f + 2u};
+      if (PAT != 2) {
+        unsigned* x = reinterpret_cast<unsigned*>(xyz + 12 * i);
+        if (kNtXyz) {
+          __builtin_nontemporal_store(f, x);
+          __builtin_nontemporal_store(f + 1u, x + 1);
+          __builtin_nontemporal_store(f + 2u, x + 2);
+        } else {
+          *reinterpret_cast<v3u*>(x) = v3u{f, f + 1u, f + 2u};
+        }
+      }
       if (PAT != 1) {
-        *reinterpret_cast<uint16_t*>(bgr + 3 * i) = static_cast<uint16_t>(f);
-        bgr[3 * i + 2] = static_cast<uint8_t>(f >> 16);
+        if (kNtBgr) {
+          __builtin_nontemporal_store(static_cast<uint16_t>(f), reinterpret_cast<uint16_t*>(bgr + 3 * i));
+          __builtin_nontemporal_store(static_cast<uint8_t>(f >> 16), bgr + 3 * i + 2);
+        } else {
+          *reinterpret_cast<uint16_t*>(bgr + 3 * i) = static_cast<uint16_t>(f);
+          bgr[3 * i + 2] = static_cast<uint8_t>(f >> 16);
+        }
       }
     }
   }
@@ -73,7 +93,7 @@ int main(int argc, char** argv) {
   (void)hipEventCreate(&b);
   for (int per_cu : {4, 8}) {
     const int gx = per_cu * n_cu;
-    for (int pat = 0; pat <= 4; ++pat) {
+    for (int pat = 0; pat <= 8; ++pat) {
       float best = 1e30f, sum = 0.f;
       for (int r = 0; r < 23; ++r) {
         (void)hipEventRecord(a, 0);
@@ -82,7 +102,11 @@ int main(int argc, char** argv) {
           case 1: hipLaunchKernelGGL(pts_k<1>, dim3(gx), dim3(256), 0, 0, xyz, bgr, side, npts, nside, sink); break;
           case 2: hipLaunchKernelGGL(pts_k<2>, dim3(gx), dim3(256), 0, 0, xyz, bgr, side, npts, nside, sink); break;
           case 3: hipLaunchKernelGGL(pts_k<3>, dim3(gx), dim3(256), 0, 0, xyz, bgr, side, npts, nside, sink); break;
-          default: hipLaunchKernelGGL(pts_k<4>, dim3(gx), dim3(256), 0, 0, xyz, bgr, side, npts, nside, sink);
+          case 4: hipLaunchKernelGGL(pts_k<4>, dim3(gx), dim3(256), 0, 0, xyz, bgr, side, npts, nside, sink); break;
+          case 5: hipLaunchKernelGGL(pts_k<5>, dim3(gx), dim3(256), 0, 0, xyz, bgr, side, npts, nside, sink); break;
+          case 6: hipLaunchKernelGGL(pts_k<6>, dim3(gx), dim3(256), 0, 0, xyz, bgr, side, npts, nside, sink); break;
+          case 7: hipLaunchKernelGGL(pts_k<7>, dim3(gx), dim3(256), 0, 0, xyz, bgr, side, npts, nside, sink); break;
+          default: hipLaunchKernelGGL(pts_k<8>, dim3(gx), dim3(256), 0, 0, xyz, bgr, side, npts, nside, sink);
         }
         (void)hipEventRecord(b, 0);
         if (hipEventSynchronize(b) != hipSuccess) return 3;
@@ -94,7 +118,7 @@ int main(int argc, char** argv) {
         }
       }
       const double wbytes = pat == 1 ? 12.0 * npts : pat == 2 ? 3.0 * npts : 15.0 * npts;
-      const double rbytes = pat == 4 ? 16.0 * nside : 0.0;
+      const double rbytes = pat == 4 || pat == 8 ? 16.0 * nside : 0.0;
       const double avg = sum / 20.0;
       printf("{\"views\": %d, \"points\": %lld, \"wg_per_cu\": %d, \"pattern\": %d, \"best_us\": %.2f, \"avg_us\": %.2f, "
              "\"write_GBps\": %.0f, \"total_GBps\": %.0f}\n",

@@ -55,7 +55,14 @@ __global__ __launch_bounds__(256) void planar_rw(const uint8_t* st, int64_t HW, 
 
 // the same traffic with each store instruction writing 1 KB contiguous per
 // wave (lane l -> bytes 16 l of the instruction's 1 KB), as an LDS transpose
-// of the maps would
+// of the maps would; NT: the maps with nontemporal stores (the library since
+// round 5), the records write-through (sc1), as k_decode issues them
+template <bool NT>
+__device__ inline void st_map(v4u* p, v4u v) {
+  if (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <bool NT>
 __global__ __launch_bounds__(256) void planar_rw_contig(const uint8_t* st, int64_t HW, unsigned* out, int ngroups,
                                                         v4u* col, v4u* row, v4u* rec, v4u* msk) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -72,13 +79,19 @@ __global__ __launch_bounds__(256) void planar_rw_contig(const uint8_t* st, int64
     const int64_t c4 = chunk * kChunk / 4;  // the chunk's first v4u of a 4 B/px map
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      col[c4 + 64 * i + lane] = a + i;
-      row[c4 + 64 * i + lane] = b + i;
+      st_map<NT>(col + c4 + 64 * i + lane, a + i);
+      st_map<NT>(row + c4 + 64 * i + lane, b + i);
     }
     const int64_t c8 = chunk * kChunk / 8;
-    rec[c8 + lane] = a ^ b;
-    rec[c8 + 64 + lane] = a - b;
-    msk[chunk * kChunk / 16 + lane] = a & b;
+    if (NT) {
+      const auto rr = __builtin_amdgcn_make_buffer_rsrc(rec + c8, 0, 2048, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b128(a ^ b, rr, 16 * lane, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(a - b, rr, 1024 + 16 * lane, 0, 16);
+    } else {
+      rec[c8 + lane] = a ^ b;
+      rec[c8 + 64 + lane] = a - b;
+    }
+    st_map<NT>(msk + chunk * kChunk / 16 + lane, a & b);
   }
 }
 
@@ -159,7 +172,7 @@ int main() {
       hipMalloc(&rec, 2 * kHW) != hipSuccess || hipMalloc(&msk, kHW) != hipSuccess) return 1;
   for (int per_cu : {2, 3, 4, 8}) {
     const int grid = per_cu * n_cu;
-    for (int k = 0; k < 6; ++k) {
+    for (int k = 0; k < 7; ++k) {
       float best = 1e30f;
       for (int r = 0; r < 20; ++r) {
         (void)hipEventRecord(a, 0);
@@ -168,7 +181,8 @@ int main() {
         if (k == 2) hipLaunchKernelGGL(linear, dim3(grid), dim3(256), 0, 0, reinterpret_cast<const v4u*>(st), bytes / 16, out);
         if (k == 3) hipLaunchKernelGGL(planar_rw, dim3(grid), dim3(256), 0, 0, st, kHW, out, ngroups, col, row, rec, msk);
         if (k == 5) hipLaunchKernelGGL(quad_rw, dim3(grid), dim3(256), 0, 0, st, kHW, out, ngroups, col, row, rec, msk);
-        if (k == 4) hipLaunchKernelGGL(planar_rw_contig, dim3(grid), dim3(256), 0, 0, st, kHW, out, ngroups, col, row, rec, msk);
+        if (k == 4) hipLaunchKernelGGL(planar_rw_contig<false>, dim3(grid), dim3(256), 0, 0, st, kHW, out, ngroups, col, row, rec, msk);
+        if (k == 6) hipLaunchKernelGGL(planar_rw_contig<true>, dim3(grid), dim3(256), 0, 0, st, kHW, out, ngroups, col, row, rec, msk);
         (void)hipEventRecord(b, 0);
         (void)hipEventSynchronize(b);
         float ms = 0.f;
@@ -177,7 +191,7 @@ int main() {
       }
       const double moved = k >= 3 ? bytes + 11.0 * kHW : bytes;
       printf("{\"pattern\": \"%s\", \"wg_per_cu\": %d, \"us\": %.2f, \"GBps\": %.0f}\n",
-             k == 0 ? "planar" : k == 1 ? "tiled" : k == 2 ? "linear" : k == 3 ? "planar+kdecode_writes" : k == 4 ? "planar+contiguous_writes" : "quad+contiguous_writes", per_cu, best * 1e3,
+             k == 0 ? "planar" : k == 1 ? "tiled" : k == 2 ? "linear" : k == 3 ? "planar+kdecode_writes" : k == 4 ? "planar+contiguous_writes" : k == 5 ? "quad+contiguous_writes" : "planar+contiguous_writes_nt", per_cu, best * 1e3,
              moved / (best * 1e-3) / 1e9);
     }
   }

@@ -579,22 +579,25 @@ class ReconstructorPool:
             e.reserve(max_views, max_px)
 
     def decode_triangulate(self, stack: torch.Tensor, n_cols: int = 1920, n_rows: int = 1080, *,
-                           wait_inputs: bool = True, **kw):
+                           wait_inputs: bool = True, lane: int | None = None, **kw):
         """``Reconstructor.decode_triangulate`` on the next lane (same
         arguments; ``stream`` is the lane's own and ``out`` the lane's buffers
         when the pool reuses outputs).  ``wait_inputs=False`` skips the wait
         on the caller's stream and the allocator bookkeeping for inputs the
         caller knows are ready and kept alive (e.g. resident stacks).
-        ``next_stack``: the stack of THIS LANE's next call (``lanes`` calls
-        later), as Reconstructor.decode_triangulate's.  With
+        ``lane``: run on that lane (the round-robin continues after it)
+        instead of the next one.  ``next_stack``: the stack of THIS LANE's
+        next call, as Reconstructor.decode_triangulate's.  With
         ``wait_inputs=False`` an explicit ``out`` dict (the caller's buffers
         for this argument set, e.g. one per resident view) takes the prepared
         path too; the caller then also guarantees that no other lane writes
         those buffers meanwhile."""
         if "stream" in kw:
             raise ValueError("ReconstructorPool picks the stream (one per lane)")
+        if lane is not None and not 0 <= lane < len(self.engines):
+            raise ValueError(f"lane {lane} out of range (0..{len(self.engines) - 1})")
         with self._lock:
-            i = self._next
+            i = self._next if lane is None else lane
             self._next = (i + 1) % len(self.engines)
         eng, st = self.engines[i], self.streams[i]
         if wait_inputs:

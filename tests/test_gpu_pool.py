@@ -87,6 +87,15 @@ def test_pool_resident_inputs():
     for lane in (0, 1):
         for a, b in zip(_host(last[lane]), want[lane]):
             np.testing.assert_array_equal(a, b)
+    # an explicit lane: that lane runs it, the round-robin continues after it
+    r = pool.decode_triangulate(views[1][0], rig.Wp, rig.Hp, texture=views[1][1], maps=True, cloud=True,
+                                fast_f32=True, wait_inputs=False, lane=1)
+    assert r["lane"] == 1 and pool._next == 0
+    pool.sync()
+    for a, b in zip(_host(r), want[1]):
+        np.testing.assert_array_equal(a, b)
+    with pytest.raises(ValueError):
+        pool.decode_triangulate(views[0][0], rig.Wp, rig.Hp, texture=views[0][1], lane=2)
     pool.close()
 
 
@@ -205,7 +214,7 @@ def test_pool_view_ring_explicit_outputs():
     res = [None] * 4
     for i in range(8):
         v = i % 4
-        assert pool._next == i % 2
+        assert pool._next == i % 2  # round-robin
         res[v] = pool.decode_triangulate(views[v][0], 1920, 1080, texture=views[v][1], maps=True, cloud=True,
                                          xyz_dtype=torch.float32, wait_inputs=False, out=outs[v],
                                          next_stack=views[(v + 2) % 4][0])
@@ -249,9 +258,9 @@ def test_pool_lanes_captured_in_one_graph():
 
     def step(i):
         v = i % 4
-        pool._next = i % 2
         res[v] = pool.decode_triangulate(views[v][0], 1920, 1080, texture=views[v][1], maps=True, cloud=True,
-                                         wait_inputs=False, out=outs[v], next_stack=views[(v + 2) % 4][0])
+                                         wait_inputs=False, out=outs[v], next_stack=views[(v + 2) % 4][0],
+                                         lane=i % 2)
 
     cur = torch.cuda.Stream()
     with torch.cuda.stream(cur):
