@@ -1687,16 +1687,50 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
   };
   float* const wx = static_cast<float*>(p.xyz) + 3 * base;  // the chunk's first point (wave-uniform)
   uint8_t* const wc = p.bgr + 3 * base;
-  // (The colours leave as a short and a byte store per point.  Round 5
-  // measured the register-only form -- every 64 points' 192 colour bytes
-  // assembled by lane permutes into 48 aligned dwords, one store instruction
-  // -- and it was slower: c2 124.1-125.4 -> 127.3-127.4 us per step, c5 3.554
-  // -> 3.671 ms, same box (profiles/r05_ab/colour_pack_lines.jsonl).)
   // The xyz leave with nt stores, like k_decode's maps: nothing in the path
   // reads them back, and default-policy lines would push the records, the
   // texture and the next view's planes out of L2 / the Infinity Cache (c3-c5
   // 3-5 % faster per call, c2 3 %; nt colours gained nothing more:
   // profiles/r05_ab/nt_stores_lines.jsonl).
+  // Colours by quads, ahead of the point arithmetic: a lane takes 4
+  // consecutive points, whose 12 colour bytes start on a 4-byte boundary
+  // (point m of the chunk sits at wc + 3 m: m = (wc mod 4) + 4 k), and puts
+  // them out as one dwordx3 -- 768 contiguous bytes per store instruction,
+  // the xyz stores' shape, one instruction per 256 points.  The <= 3 points
+  // before the first quad and the <= 3 after the last go out byte by byte.
+  // (Per point, a short and a byte store per lane had cost 4x the xyz per
+  // byte; quads: c2 113.9-114.2 -> 112.3-112.7 us per step, c3 632.9 ->
+  // 615.7 us, c4 4.047 -> 3.985 ms, c5 3.183 -> 3.146 ms, two alternating
+  // runs on one box, profiles/r05_ab/colour_quad_lines.jsonl.  The
+  // register-only form -- 64 points' 192 bytes assembled by lane permutes
+  // into 48 dwords -- had been slower: colour_pack_lines.jsonl.)
+  {
+    const int a = static_cast<int>(reinterpret_cast<uintptr_t>(wc) & 3u);  // wave-uniform
+    const int head = min(a, total);
+    const int nq = total > a ? (total - a) >> 2 : 0;
+    const int t0 = a + 4 * nq;
+    int ep = -1;
+    if (lane < head) ep = lane;
+    else if (lane >= 4 && lane - 4 < total - max(t0, head)) ep = t0 + lane - 4;
+    if (ep >= 0) {
+      const uint32_t c = point_bgr(static_cast<int>(s_ent[ep] & 1023u));
+      uint8_t* cc = at_bytes(wc, 3u * static_cast<unsigned>(ep));
+      cc[0] = static_cast<uint8_t>(c);
+      cc[1] = static_cast<uint8_t>(c >> 8);
+      cc[2] = static_cast<uint8_t>(c >> 16);
+    }
+    for (int k = lane; k < nq; k += 64) {
+      const int m = a + 4 * k;
+      const uint32_t c0 = point_bgr(static_cast<int>(s_ent[m] & 1023u));
+      const uint32_t c1 = point_bgr(static_cast<int>(s_ent[m + 1] & 1023u));
+      const uint32_t c2 = point_bgr(static_cast<int>(s_ent[m + 2] & 1023u));
+      const uint32_t c3 = point_bgr(static_cast<int>(s_ent[m + 3] & 1023u));
+      uint32_t* q = reinterpret_cast<uint32_t*>(at_bytes(wc, 3u * static_cast<unsigned>(m)));  // 4-byte aligned
+      q[0] = c0 | (c1 << 24);
+      q[1] = (c1 >> 8) | (c2 << 16);
+      q[2] = (c2 >> 16) | (c3 << 8);
+    }
+  }
   for (int j0 = 0; j0 < total; j0 += 64 * kP) {
     if (mode & M_FAST32) {
       // SL_XYZ_F32_FAST (Oc = 0, pinhole rays, no pose; host-checked): the
@@ -1707,12 +1741,10 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
       // ("f32-fast").
       float fx[kP], fy[kP];
       float4 fp[kP];
-      uint32_t bgr[kP];
 #pragma unroll
       for (int i = 0; i < kP; ++i) {
         const int j = min(j0 + 64 * i + lane, total - 1);
         const uint32_t e = s_ent[j];
-        bgr[i] = point_bgr(static_cast<int>(e & 1023u));
         int uu, vv;
         chunk_uv<VEC>(u_c, v_c, e, W, &uu, &vv);
         fx[i] = *at_bytes(p.xn32, 4u * static_cast<unsigned>(uu));
@@ -1752,23 +1784,17 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           __builtin_nontemporal_store(X, xyz);
           __builtin_nontemporal_store(Y, xyz + 1);
           __builtin_nontemporal_store(Z, xyz + 2);
-          uint8_t* cc = at_bytes(wc, 3u * static_cast<unsigned>(j));
-          cc[0] = static_cast<uint8_t>(bgr[i]);
-          cc[1] = static_cast<uint8_t>(bgr[i] >> 8);
-          cc[2] = static_cast<uint8_t>(bgr[i] >> 16);
         }
       }
       continue;
     }
     double ra[kP], rb[kP], rcz[kP];  // pinhole: x, y, -; Nc: r0, r1, r2
     double4 pl[kP];
-    uint32_t bgr[kP];
 #pragma unroll
     for (int i = 0; i < kP; ++i) {
       const int j = min(j0 + 64 * i + lane, total - 1);  // past the end: repeat the last point
       const uint32_t e = s_ent[j];
       const int local = static_cast<int>(e & 1023u);
-      bgr[i] = point_bgr(local);
       if (mode & M_NC) {
         const int64_t q = cpx + local;
         ra[i] = p.nc_rays[q];
@@ -2005,10 +2031,6 @@ __device__ __forceinline__ void cloud_points(const Params& p, int view, int64_t 
           __builtin_nontemporal_store(static_cast<float>(Y[i]), xyz + 1);
           __builtin_nontemporal_store(static_cast<float>(Z[i]), xyz + 2);
         }
-        uint8_t* cc = at_bytes(wc, 3u * o);
-        cc[0] = static_cast<uint8_t>(bgr[i]);
-        cc[1] = static_cast<uint8_t>(bgr[i] >> 8);
-        cc[2] = static_cast<uint8_t>(bgr[i] >> 16);
       }
     }
   }
