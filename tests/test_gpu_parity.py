@@ -487,6 +487,39 @@ def test_time_kernels_keeps_outputs_and_later_calls_exact(eng):
         eng.time_kernels(3)  # nothing left to re-run
 
 
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_colour_quads_any_caller_alignment(eng, shift):
+    """k_cloud's colour quads (4 consecutive points per lane, one dwordx3) take
+    the quad phase from the colour buffer's byte address: a caller's bgr buffer
+    at every address mod 4, two views (the second view's chunks start at other
+    phases), maps + cloud and cloud only -- colours, xyz and offsets equal to
+    the oracle's (sl_system.py:651, C = texture[idx])."""
+    rig, st0, tex0, cal = _render(96, 256, 1920, 1080, seed=41)
+    _, st1, tex1, _ = _render(96, 256, 1920, 1080, seed=42, view=10.0)
+    st = torch.stack([st0, st1])
+    tx = torch.stack([tex0, tex1])
+    eng.set_calibration(cal, 96, 256)
+    cap = 2 * 96 * 256
+    for maps in (True, False):
+        big = torch.full((3 * cap + 8,), 0xA5, dtype=torch.uint8, device="cuda")
+        bgr = big[shift:shift + 3 * cap].view(cap, 3)
+        out = {"xyz": torch.empty((cap, 3), dtype=torch.float32, device="cuda"), "bgr": bgr,
+               "view_offsets": torch.empty(3, dtype=torch.int64, device="cuda")}
+        res = eng.decode_triangulate(st, 1920, 1080, texture=tx, maps=maps, cloud=True, out=out)
+        eng.sync()
+        assert res["cloud"].bgr.data_ptr() == big.data_ptr() + shift
+        xyz, col, off = _cloud_np(res["cloud"])
+        for v, (s_, t_) in enumerate(((st0, tex0), (st1, tex1))):
+            _, _, _, P, C = o.decode_triangulate(list(s_.cpu().numpy()), t_.cpu().numpy(), cal)
+            assert off[v + 1] - off[v] == len(P)
+            np.testing.assert_array_equal(col[off[v]:off[v + 1]], C)
+            _assert_f32(xyz[off[v]:off[v + 1]], P)
+        tail = big[shift + 3 * int(off[-1]):].cpu().numpy()
+        assert np.all(tail == 0xA5), "bytes past the cloud were written"
+        if shift:
+            assert np.all(big[:shift].cpu().numpy() == 0xA5), "bytes before the buffer were written"
+
+
 def test_full_12mp_posed_views_cloud_only_vs_oracle(eng):
     """Config 4/5 shapes at full size: two 4000x3000 views (12 MP, 11+11 bits,
     cloud only: the row planes are never read) with the turntable pose
