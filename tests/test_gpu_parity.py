@@ -487,13 +487,16 @@ def test_time_kernels_keeps_outputs_and_later_calls_exact(eng):
         eng.time_kernels(3)  # nothing left to re-run
 
 
-@pytest.mark.parametrize("shift", [0, 1, 2, 3])
-def test_colour_quads_any_caller_alignment(eng, shift):
+@pytest.mark.parametrize("shift", [0, 16, 48])
+def test_colour_quads_caller_buffers(eng, shift):
     """k_cloud's colour quads (4 consecutive points per lane, one dwordx3) take
-    the quad phase from the colour buffer's byte address: a caller's bgr buffer
-    at every address mod 4, two views (the second view's chunks start at other
-    phases), maps + cloud and cloud only -- colours, xyz and offsets equal to
-    the oracle's (sl_system.py:651, C = texture[idx])."""
+    the quad phase from the chunk's first colour byte address, 3 x its first
+    point's index (every phase mod 4 occurs across a frame's chunks), with the
+    points before the first quad and after the last stored byte by byte: two
+    views, maps + cloud and cloud only, caller buffers at several 16-byte
+    aligned offsets -- colours, xyz and offsets equal to the oracle's
+    (sl_system.py:651, C = texture[idx]), no byte outside the cloud written.
+    A buffer that is not 16-byte aligned is refused (sl_decode_triangulate)."""
     rig, st0, tex0, cal = _render(96, 256, 1920, 1080, seed=41)
     _, st1, tex1, _ = _render(96, 256, 1920, 1080, seed=42, view=10.0)
     st = torch.stack([st0, st1])
@@ -501,7 +504,7 @@ def test_colour_quads_any_caller_alignment(eng, shift):
     eng.set_calibration(cal, 96, 256)
     cap = 2 * 96 * 256
     for maps in (True, False):
-        big = torch.full((3 * cap + 8,), 0xA5, dtype=torch.uint8, device="cuda")
+        big = torch.full((3 * cap + 64,), 0xA5, dtype=torch.uint8, device="cuda")
         bgr = big[shift:shift + 3 * cap].view(cap, 3)
         out = {"xyz": torch.empty((cap, 3), dtype=torch.float32, device="cuda"), "bgr": bgr,
                "view_offsets": torch.empty(3, dtype=torch.int64, device="cuda")}
@@ -518,6 +521,12 @@ def test_colour_quads_any_caller_alignment(eng, shift):
         assert np.all(tail == 0xA5), "bytes past the cloud were written"
         if shift:
             assert np.all(big[:shift].cpu().numpy() == 0xA5), "bytes before the buffer were written"
+    assert len(P) > 1000  # 48 chunks over both views: many quads, heads and tails
+    big = torch.empty((3 * cap + 8,), dtype=torch.uint8, device="cuda")
+    bad = {"xyz": torch.empty((cap, 3), dtype=torch.float32, device="cuda"),
+           "bgr": big[1:1 + 3 * cap].view(cap, 3), "view_offsets": torch.empty(3, dtype=torch.int64, device="cuda")}
+    with pytest.raises(ValueError):
+        eng.decode_triangulate(st, 1920, 1080, texture=tx, maps=False, cloud=True, out=bad)
 
 
 def test_full_12mp_posed_views_cloud_only_vs_oracle(eng):
