@@ -138,8 +138,6 @@ def parse(argv=None):
                     help="N > 1: also time BASELINE config 3 strong-scaled (36 views sharded over the N ranks) "
                          "and report it in multi_gpu.strong_c3 (default)")
     ap.add_argument("--no-strong-leg", dest="strong_leg", action="store_false")
-    ap.add_argument("--lane-priority", dest="lane_priority", action="store_true",
-                    help="measurement: lane 0's stream at high priority (hipStreamCreateWithPriority)")
     ap.add_argument("--ring", type=int, default=None,
                     help="one view in flight: the headline window cycles through this many distinct resident "
                          "views (stack, texture and outputs each), chained; 1 = the same view every step.  Default "
@@ -695,8 +693,6 @@ def main():
     pool = None
     if S > 1:
         pool = core.ReconstructorPool(dev, lanes=S, reuse_outputs=True)
-        if a.lane_priority:  # measurement: lane 0 on a high-priority stream, the others default
-            pool.streams = [torch.cuda.Stream(dev, priority=(-1 if i == 0 else 0)) for i in range(S)]
         pool.set_calibration(calib, H, W)
         pool.reserve(V, H * W)
         eng = pool.engines[0]
