@@ -150,7 +150,7 @@ def parse(argv=None):
                          "(0: off)")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
-                         "scripts/traffic_from_pmc.py); default profiles/r05_traffic2/traffic_<config>.json")
+                         "scripts/traffic_from_pmc.py); default profiles/r05_traffic3/traffic_<config>.json")
     return ap.parse_args(argv)
 
 
@@ -1051,7 +1051,7 @@ def main():
         # of the same command, from a committed profile -- not measured here
         traffic = traffic_k = None
         if a.traffic is None:
-            a.traffic = os.path.join(REPO, "profiles", "r05_traffic2", f"traffic_{a.config}.json")
+            a.traffic = os.path.join(REPO, "profiles", "r05_traffic3", f"traffic_{a.config}.json")
         if os.path.exists(a.traffic):
             try:
                 tj = json.load(open(a.traffic))
