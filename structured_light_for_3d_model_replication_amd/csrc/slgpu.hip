@@ -192,7 +192,7 @@ struct Params {
   unsigned* super_par;     // [0]: the buffer the next producer accumulates into, [1]: the one k_cloud reads
   int sb_shift;
   int rerun;               // sl_time_kernels' re-runs: consumers leave their inputs as they are
-  int cloud_gx;            // k_cloud: workgroups per view that triangulate (the grid's x beyond: pre-stats)
+  int cloud_gx;            // k_cloud: workgroups per view that triangulate (the grid's first x: pre-stats)
   // k_cloud's pre-stats workgroups (sl_stack_next): the NEXT call's histogram
   // pass (k_stats' work) for the views of its first launch group, beside this
   // call's triangulation; null pre_stack: none
@@ -660,9 +660,9 @@ __device__ __forceinline__ unsigned* super_produce(const Params& p) {
   }
   return p.super_base + sel * kSuperCap;
 }
-__device__ __forceinline__ const unsigned* super_consume(const Params& p) {
+__device__ __forceinline__ const unsigned* super_consume(const Params& p, int bx) {
   const unsigned sel = p.super_par[1] & 1u;
-  if (!p.rerun && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) p.super_par[0] = sel ^ 1u;
+  if (!p.rerun && bx == 0 && blockIdx.y == 0 && threadIdx.x == 0) p.super_par[0] = sel ^ 1u;
   return p.super_base + sel * kSuperCap;
 }
 constexpr int kDecodeLds = (kDecPlWords + kDecX) * 4;  // bytes: > the histogram replicas
@@ -2144,18 +2144,23 @@ __global__ __launch_bounds__(kThreads, 5) void k_cloud(Params p) {
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, provably
   const int view = blockIdx.y;
-  // pre-stats (sl_stack_next): the workgroups past cloud_gx compute the next
-  // call's (or launch group's) histograms, after the triangulating ones
-  const int cx = blockIdx.x;  // triangulating workgroup index in the view
-  if (cx >= p.cloud_gx) {
-    pre_stats_block(p, cx - p.cloud_gx, gridDim.x - p.cloud_gx, &s_ent[0][0], reinterpret_cast<int*>(s_wred));
+  // pre-stats (sl_stack_next): the first gridDim.x - cloud_gx workgroups of
+  // each row compute the next call's (or launch group's) histograms; the
+  // triangulating ones follow.  (Ahead of them, the pass runs beside the
+  // first triangulating workgroups, and the launch ends with the
+  // triangulation's own tail: c5 -1.1 %, c2 / c3 -0.2-0.3 % against the pass
+  // after them, two alternating runs, profiles/r05_ab/pre_stats_front_lines.jsonl)
+  const int npre = static_cast<int>(gridDim.x) - p.cloud_gx;
+  if (static_cast<int>(blockIdx.x) < npre) {
+    pre_stats_block(p, blockIdx.x, npre, &s_ent[0][0], reinterpret_cast<int*>(s_wred));
     return;
   }
+  const int cx = static_cast<int>(blockIdx.x) - npre;  // triangulating workgroup index in the view
   const int civ = cx * kWaves + wid;
   const int64_t b = static_cast<int64_t>(view) * p.cloud_gx + cx;  // block index in the launch
   const int64_t gc = static_cast<int64_t>(view) * p.cpv + civ;
   const int before = (lane < wid && civ < p.cpv) ? p.chunk_counts[gc - wid + lane] : 0;  // earlier waves' chunks
-  long long base = block_offset(p, super_consume(p), b, tid, lane, wid, s_wred);
+  long long base = block_offset(p, super_consume(p, cx), b, tid, lane, wid, s_wred);
   base += p.base_in ? *p.base_in : 0ll;
   base += wave_sum(before);
   base = uniform64(base);
@@ -2545,7 +2550,7 @@ int launch_groups(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int co
     ev = &c->prof_ev[kProfEv * c->prof_n++];
   // The pre-stats workgroups' arguments on launch parameters pc of a grid
   // with nv rows, for the pnv views of stack pst (view stride pvs): the launch
-  // grows by as many workgroups per row as they need (after its own); the
+  // grows by as many workgroups per row as they need (ahead of its own); the
   // pass accumulates into the (clean) histogram buffer.
   auto add_pre = [&](Params& pc, dim3& grid, int nv, const uint8_t* pst, int64_t pvs, int pnv) {
     const int64_t bpv = pre_bpv_of(pnv);
