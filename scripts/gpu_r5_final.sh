@@ -1,6 +1,7 @@
 # Round-5 evidence at HEAD, one box (run through gpurun):
 #   bash scripts/gpu_r5_final.sh OUT
-# 1. calibrated PMC traffic per config (gpu_r4_traffic.sh -> gpurun_out/OUT_traffic/);
+# 1. calibrated PMC traffic per config (gpu_r4_traffic.sh -> gpurun_out/OUT_traffic/; SKIP_TRAFFIC=1:
+#    the committed profiles/r05_traffic3/ files instead);
 # 2. the GPU suite and smoke;
 # 3. the driver's default bench command, then every config's bench line, each
 #    followed by rocprofv3 --kernel-trace --stats of the same command (gpu_r4.sh
@@ -10,7 +11,11 @@ set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=$1
 T=gpurun_out/${O}_traffic
-bash scripts/gpu_r4_traffic.sh ${O}_traffic c2:32 c3:10 c4:3 c5:4 || exit 1
+if [ "${SKIP_TRAFFIC:-0}" = 1 ]; then  # the committed traffic files (the bytes did not change)
+  T=profiles/r05_traffic3
+else
+  bash scripts/gpu_r4_traffic.sh ${O}_traffic c2:32 c3:10 c4:3 c5:4 || exit 1
+fi
 NB="--no-cpu-baseline --no-secondary --single-shot 0"
 bash scripts/gpu_r4.sh $O \
   "tests|suite||tests" \
