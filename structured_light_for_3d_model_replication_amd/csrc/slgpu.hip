@@ -2219,7 +2219,7 @@ struct sl_ctx {
   int64_t cap_codes = 0;
   int last_views = 0;
   int decode_wgs = 0;  // k_decode grid cap in workgroups over all views
-  int pre_wgs = 0;     // pre-stats workgroups of a pass (8 per CU)
+  int pre_wgs = 0;     // pre-stats workgroups of a pass (2 per CU)
   // optional per-call HIP-event timing of k_decode / k_count / k_cloud
   std::vector<hipEvent_t> prof_ev;  // kProfEv events per call slot
   std::vector<int> prof_groups;     // launch groups recorded per call
@@ -2533,9 +2533,12 @@ int launch_groups(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int co
     if (r) return r;
   }
   if (!pre_use) hist_dirty = 0;
-  // pre-stats workgroups per view of a pass over nv views: 8 per CU in all
-  // (one 16-pixel step per thread at config 2; measured 0.5-1 us faster per c2
-  // step than k_stats' 2 per CU)
+  // pre-stats workgroups per view of a pass over nv views: 2 per CU in all,
+  // k_stats' size (4 steps of 16 pixels per thread at config 2).  Round 3,
+  // with the pass after the triangulating workgroups, 8 per CU had been
+  // 0.5-1 us faster per c2 step; ahead of them, 2 per CU is: c2 111.7 / 111.3
+  // -> 110.7 / 110.1 us, c5 3.211 / 3.212 -> 3.190 / 3.190 ms (4 per CU in
+  // between), profiles/r05_ab/pre_stats_size_front_lines.jsonl
   auto pre_bpv_of = [&](int nv) -> int64_t {
     const int64_t per_view = (p0.HW / 16 + kThreads - 1) / kThreads;
     return std::max<int64_t>(1, std::min<int64_t>(per_view, (c->pre_wgs + nv - 1) / nv));
@@ -2870,7 +2873,7 @@ int sl_ctx_create(int device, sl_ctx** out) {
     n_cu = 256;
   c->n_cu = n_cu;
   c->decode_wgs = kDecodePerCu * n_cu;
-  c->pre_wgs = 8 * n_cu;
+  c->pre_wgs = 2 * n_cu;
   // (test switch: the exact f32 mode through the reference's own operation
   // sequence instead of the verified route, which the GPU tests compare)
   if (const char* d = getenv("SLGPU_VERIFY32")) c->verify32 = atoi(d) != 0;
