@@ -55,6 +55,8 @@ sys.path.insert(0, REPO)
 from structured_light_for_3d_model_replication_amd import core, parallel, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# the committed calibrated-PMC traffic profiles the lines cite (scripts/gpu_r4_traffic.sh)
+TRAFFIC_DIR = os.path.join("profiles", "r05_traffic3")
 
 CONFIGS = {
     # BASELINE.json configs.  views = views per GPU per step (weak scaling;
@@ -64,7 +66,8 @@ CONFIGS = {
     # 360-view scan over 8 GPUs (24.8 / 17.2 GB of stacks resident in HBM);
     # c3: the 36-view turntable scan (strong scaling shards it).
     "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0,
-               streams=3),  # with next-stats (2 launches per call): 3 lanes best
+               streams=3,  # with next-stats (2 launches per call): 3 lanes best
+               ring_control=12),  # the control window's distinct views: 12 x 23 MB > the 256 MiB Infinity Cache
     "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0,
                ring=3, streams=2),  # distinct resident views cycled (no Infinity-Cache
                                     # carry-over; 3 rounded up to 4, a multiple of the lanes), 2 lanes (5.2)
@@ -143,14 +146,14 @@ def parse(argv=None):
                          "views (stack, texture and outputs each), chained; 1 = the same view every step.  Default "
                          "(CONFIGS): c2 3 -- one view's texture, records and outputs stayed in the 256 MB Infinity "
                          "Cache from step to step and made the one-view window 3.5 %% faster (DESIGN.md 6.1)"),
-    ap.add_argument("--ring-control", dest="ring_control", type=int, default=3,
+    ap.add_argument("--ring-control", dest="ring_control", type=int, default=None,
                     help="one view in flight: a second window with this many distinct views when the headline "
                          "uses one (or one view when the headline cycles several), reported in "
                          "timing.distinct_views -- does the 256 MB Infinity Cache help the one-view window? "
-                         "(0: off)")
+                         "(default per config: c1 12 -- 12 x 23 MB of inputs exceed the cache --, else 3; 0: off)")
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
-                         "scripts/traffic_from_pmc.py); default profiles/r05_traffic3/traffic_<config>.json")
+                         "scripts/traffic_from_pmc.py); default " + TRAFFIC_DIR + "/traffic_<config>.json")
     return ap.parse_args(argv)
 
 
@@ -225,7 +228,10 @@ def gather_report(el_s: float, n_local: int, bytes_per_point: int, device, gathe
     moved = sum(c for r, c in enumerate(counts) if r != 0) * bytes_per_point
     rep.update({"gather_counts": [int(c) for c in counts], "gather_counts_len": len(counts),
                 "gather_bytes_to_root": int(moved), "gather_ms": 1e3 * g_s,
-                "gather_GBps": moved / g_s / 1e9 if g_s > 0 else None})
+                "gather_GBps": moved / g_s / 1e9 if g_s > 0 else None,
+                # what the gather must move, from every rank's point count before it ran
+                "expected_gather_bytes_to_root": int(sum(per_rank_pts[1:]) * bytes_per_point),
+                "bytes_per_point": bytes_per_point})
     return rep
 
 
@@ -290,6 +296,12 @@ def _stand_in_leg(a, views3, leg_step):
     return el, xyz, torch.zeros((xyz.shape[0], 3), dtype=torch.uint8)
 
 
+def ideal_strong_efficiency(V: int, world: int) -> float:
+    """The bound contiguous view shards put on strong-scaling efficiency:
+    V / (N x the largest shard) (36 views: 1.0 at N = 2, 3, 4; 0.9 at N = 8)."""
+    return V / (world * max(len(parallel.shard_views(V, world, r)) for r in range(world)))
+
+
 def strong_leg_report(a, world, rank, distributed, device, px_per_view, run, V=36):
     """BASELINE config 3 as the N-GPU run's second line: V views in total,
     sharded over the ranks (parallel.shard_views, view v -> rank
@@ -310,6 +322,12 @@ def strong_leg_report(a, world, rank, distributed, device, px_per_view, run, V=3
     rep.update({"config": f"BASELINE config 3: {V} x 1920x1080 views in total, sharded over {world} rank(s) "
                           "(strong scaling), cloud only, exact xyz",
                 "views_total": V, "per_rank_views": per_views, "steps": a.steps,
+                # the slowest rank sets the step: V / (N x its views) is the best
+                # efficiency against one GPU that contiguous view shards allow
+                # (36 / (8 x 5) = 0.9 at N = 8), before any cost of the path
+                "ideal_strong_efficiency": ideal_strong_efficiency(V, world),
+                "ideal_strong_efficiency_note": "V / (N x max views per rank): the bound the shard imbalance "
+                                                "puts on px/s(N) / (N x px/s(1)) with per-view work constant",
                 "per_rank_ms_per_step": [1e3 * t / a.steps for t in rep["per_rank_s"]],
                 "ms_per_step": 1e3 * t_max / a.steps,
                 "px_per_s": V * px_per_view * a.steps / t_max if t_max > 0 else None})
@@ -719,8 +737,9 @@ def main():
     # outputs are always written by one lane, in order.
     ring_req = max(1, a.ring if a.ring is not None else cfg.get("ring", 1)) if V == 1 else 1
     ctl_req = 0
-    if V == 1 and a.ring_control > 0:
-        ctl_req = 1 if ring_req > 1 else a.ring_control  # the control: one view, or distinct ones
+    ring_ctl = a.ring_control if a.ring_control is not None else cfg.get("ring_control", 3)
+    if V == 1 and ring_ctl > 0:
+        ctl_req = 1 if ring_req > 1 else ring_ctl  # the control: one view, or distinct ones
     slots = [dict(stack=stack, tex=tex, out=out)]  # the distinct resident views
 
     def ring_of(n):
@@ -763,7 +782,7 @@ def main():
         # the lane's (never read while the window runs)
         res = pool.decode_triangulate(st_, n_cols, n_rows, texture=tx_, maps=maps, cloud=True,
                                       xyz_dtype=torch.float32, poses=poses, fast_f32=head_fast,
-                                      wait_inputs=False, lane=at % S, next_stack=nx_,
+                                      wait_inputs=False, lane=at % S, next_stack=nx_, prepared=True,
                                       **({"out": o_} if V == 1 else {}))
         return res["stream"]
 
@@ -890,8 +909,18 @@ def main():
         else:
             el_rank, _ = timed(a.steps)
         enq_ms = host_enq_ms[0]
+        lane_snaps = []
         if snap is not None:  # the headline window's last step (the next window's sync waits for the copies)
             snap_copy(snap, out, cur)
+            if V == 1:
+                # and every other lane's last step: the window ends on slot 0
+                # (lane 0), so lane j's last step ran slot (R - S + j) % R
+                R_h = len(head_slots)
+                for j in range(1, S):
+                    k_s = (R_h - S + j) % R_h
+                    sj = snap_alloc(head_slots[k_s]["out"], V, maps)
+                    snap_copy(sj, head_slots[k_s]["out"], cur)
+                    lane_snaps.append((j, k_s, sj))
         el_ev, step_us = timed(a.steps, evs)
         # the control window: the same K steps over ctl_R distinct resident
         # views (or one, when the headline cycles several), after its own
@@ -1023,6 +1052,16 @@ def main():
     verified, verification = None, None
     if snap is not None:
         verified, verification = verify(snap, stack, tex, poses, calib, n_cols, n_rows, head_fast)
+        if V == 1:
+            # one ring slot per lane: lane 0's last step (slot 0, above) and
+            # every other lane's, each against the oracle on its own resident view
+            lanes_v = [{"lane": 0, "slot": 0, "views": verification["views"]}]
+            for j, k_s, sj in lane_snaps:
+                okj, verj = verify(sj, head_slots[k_s]["stack"], head_slots[k_s]["tex"], poses, calib, n_cols,
+                                   n_rows, head_fast)
+                lanes_v.append({"lane": j, "slot": k_s, "views": verj["views"]})
+                verified = verified and okj
+            verification["lane_slots"] = lanes_v
         if distinct is not None and distinct.get("snap") is not None:
             ok2, ver2 = verify(distinct["snap"], stack, tex, poses, calib, n_cols, n_rows, head_fast)
             verification["distinct_views_window"] = ver2
@@ -1051,7 +1090,7 @@ def main():
         # of the same command, from a committed profile -- not measured here
         traffic = traffic_k = None
         if a.traffic is None:
-            a.traffic = os.path.join(REPO, "profiles", "r05_traffic3", f"traffic_{a.config}.json")
+            a.traffic = os.path.join(REPO, TRAFFIC_DIR, f"traffic_{a.config}.json")
         if os.path.exists(a.traffic):
             try:
                 tj = json.load(open(a.traffic))
@@ -1105,10 +1144,15 @@ def main():
                            "window": distinct["window"], "preroll": distinct["preroll"],
                            "resident_input_bytes": distinct["resident_input_bytes"],
                            "note": "the same K chained steps cycling through this many distinct resident views "
-                                   "(stack, texture and outputs each), after their own pre-roll: > 1 view puts "
-                                   "more than the 256 MB Infinity Cache between a view's steps, so no texture, "
-                                   "record or output line of a view survives to its next step; verified like "
-                                   "the headline (verification.distinct_views_window)"}},
+                                   "(stack, texture and outputs each), after their own pre-roll"
+                                   + ("; one view: what of its texture, records and outputs the 256 MiB "
+                                      "Infinity Cache keeps may serve the next step" if distinct["views"] == 1
+                                      else "; their inputs exceed the 256 MiB Infinity Cache, so no line of a "
+                                           "view's inputs survives to its next step"
+                                      if distinct["resident_input_bytes"] > 2 ** 28
+                                      else "; their inputs fit the 256 MiB Infinity Cache, so the control does "
+                                           "not exclude cache hits from step to step")
+                                   + "; verified like the headline (verification.distinct_views_window)"}},
             "roofline": {"bound": "hbm", "scope": "whole path per step: every kernel of the step",
                          "achieved": path_gbps, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": path_gbps / HBM_PEAK_GBS, "traffic": traffic,

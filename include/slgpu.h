@@ -74,14 +74,18 @@ const char* sl_ctx_last_error(const sl_ctx* ctx);
  * allocate nothing (required before stream capture into a hipGraph).  Calls
  * grow scratch on demand otherwise.
  * Graphs: any sequence of calls captured on one stream replays any number of
- * times, in any order with other work on the context.  The scratch a launch
- * accumulates into (block sums, the adaptive mask's histograms) is zero at
- * every launch-group boundary -- the kernel that consumes it zeroes it, on the
- * device, once its last reader is done -- and the one thing that crosses a
- * call boundary, a histogram pass queued by sl_stack_next, is taken only by a
- * call in the same capture (a graph's first call therefore runs its own
- * histogram pass; a pass the graph's last call queues is cleared by the
- * next call that does not take it). */
+ * times, in any order with other work on the context.  Nothing a launch group
+ * accumulates into depends on the host's view of the sequence: the super-block
+ * sums live in two buffers whose alternation is kept on the device (the
+ * producer, k_decode or k_count, reads a selector word, accumulates into that
+ * buffer and zeroes the OTHER one, whose last reader -- the previous group's
+ * k_cloud -- is done; the consumer only flips the selector, so the buffer it
+ * read keeps its sums until the next producer zeroes it); the adaptive mask's
+ * histograms are zeroed by their last reader (an arrival counter).  The one
+ * thing that crosses a call boundary, a histogram pass queued by
+ * sl_stack_next, is taken only by a call in the same capture (a graph's first
+ * call therefore runs its own histogram pass; a pass the graph's last call
+ * queues is cleared by the next call that does not take it). */
 int sl_ctx_reserve(sl_ctx* ctx, int64_t max_views, int64_t max_px);
 
 /* Upload calibration for an H x W camera (the calib.mat fields loaded at
@@ -231,7 +235,8 @@ int sl_last_launch_info(sl_ctx* ctx, int* path, int64_t* launches, int64_t* last
  * rebuilt once first, untimed; k_cloud and k_count run first: the call's
  * outputs are rewritten with the same values.  Afterwards the context's
  * scratch is clean again: a histogram pass queued by sl_stack_next is dropped
- * (the next call computes its own). */
+ * (the next call computes its own).  Eager only: SL_EINVAL while that stream
+ * is capturing into a graph. */
 int sl_time_kernels(sl_ctx* ctx, int reps, double* decode_ms, double* count_ms, double* cloud_ms);
 
 /* ASCII PLY of a cloud exactly as the reference writes it (sl_system.py:665-691,

@@ -1,0 +1,177 @@
+"""User-visible end-to-end rate at HEAD: scan folders on disk ->
+PLY files on disk, the way the GUI and the batch GUI run them.
+
+    python scripts/e2e_bench.py [--views 6] [--formats bmp,png,jpg] [--H 2160 --W 3840]
+
+For each capture format, ``views`` 4K scan folders of 46 files (config-2 rig,
+11 + 11 bits with inverses) are written to $TMPDIR:
+  bmp   8-bit single-channel BMP (what sl_system.py:519 reads back)
+  png   8-bit single-channel PNG (the *.png fallback, sl_system.py:512-513)
+  jpg   colour JPEG bytes saved under .bmp names (server/server.py:70: the
+        Android capture's upload is written as-is)
+Legs (one JSON line each):
+  gui_stages  generate_cloud's work for one folder at a time, stage by stage
+              (median over the folders): file decoding (all 46 files + the
+              colour re-read of file 0, io.read_stack, 8 threads), H2D, the
+              kernels (k_stats, k_decode, k_cloud; f64 xyz, generate_cloud's
+              mode), D2H of the points, the ASCII PLY (sl_system.py:665-691:
+              native formatter, 16 threads) -- and SLSystem.generate_cloud's own
+              wall time for the same folders (stdout suppressed)
+  batch       SLSystem.generate_clouds over all folders (pipeline.ViewPipeline:
+              24 cloud planes decoded into pinned slots, H2D, kernels, D2H and
+              the PLY of neighbouring views overlapped): views/s, and the
+              pipeline's host-side totals
+Disk: one format's folders at a time (~2.5 GB for 6 BMP views + their PLYs).
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io as _io
+import json
+import os
+import shutil
+import statistics
+import sys
+import tempfile
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import scipy.io
+import torch
+from PIL import Image
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from structured_light_for_3d_model_replication_amd import core, io, ply, sl_system, synth  # noqa: E402
+
+
+def write_folder(folder, stack, fmt, pool):
+    os.makedirs(folder)
+
+    def one(j):
+        a = stack[j]
+        if fmt == "png":
+            Image.fromarray(a).save(os.path.join(folder, f"{j + 1:02d}.png"))
+        elif fmt == "jpg":  # colour JPEG bytes under a .bmp name (server.py:70)
+            with open(os.path.join(folder, f"{j + 1:02d}.bmp"), "wb") as f:
+                Image.fromarray(np.repeat(a[:, :, None], 3, axis=2)).save(f, format="JPEG", quality=95)
+        else:
+            Image.fromarray(a).save(os.path.join(folder, f"{j + 1:02d}.bmp"))
+    list(pool.map(one, range(len(stack))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--views", type=int, default=6)
+    ap.add_argument("--formats", default="bmp,png,jpg")
+    ap.add_argument("--H", type=int, default=2160)
+    ap.add_argument("--W", type=int, default=3840)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rig = synth.Rig(H=a.H, W=a.W)
+    cal = synth.make_calibration(rig, with_Nc=False)
+    stacks = []
+    for v in range(min(a.views, 4)):  # 4 distinct synthetic views, cycled
+        s, _ = synth.render_stack(rig, seed=3000 + v, view_deg=10.0 * v, device="cpu")
+        stacks.append(s.numpy())
+    root = tempfile.mkdtemp(prefix="sl_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+    calib_file = os.path.join(root, "calib.mat")
+    scipy.io.savemat(calib_file, {k: np.asarray(v) for k, v in cal.items()})
+    eng = core.engine(dev)
+    pool = ThreadPoolExecutor(16)
+    slsys = sl_system.SLSystem()
+    px = a.H * a.W
+    try:
+        for fmt in a.formats.split(","):
+            fdir = os.path.join(root, fmt)
+            os.makedirs(fdir)
+            t0 = time.perf_counter()
+            folders = []
+            for v in range(a.views):
+                f = os.path.join(fdir, f"scan_{v:03d}")
+                write_folder(f, stacks[v % len(stacks)], fmt, pool)
+                folders.append(f)
+            write_s = time.perf_counter() - t0
+            disk = sum(os.path.getsize(os.path.join(folders[0], x)) for x in os.listdir(folders[0]))
+            # page cache warm for every leg (the files were just written)
+            # ---- gui_stages: generate_cloud's work, stage by stage ----
+            st = {k: [] for k in ("decode_files", "h2d", "kernels", "d2h", "ply")}
+            pts = []
+            for f in folders:
+                t0 = time.perf_counter()
+                stack, texture, _ = io.read_stack(f)
+                t1 = time.perf_counter()
+                eng.set_calibration(cal, stack.shape[1], stack.shape[2])
+                ds = torch.from_numpy(stack).to(dev)
+                dt = torch.from_numpy(texture).to(dev)
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                res = eng.decode_triangulate(ds, texture=dt, maps=False, cloud=True, xyz_dtype=torch.float64)
+                eng.sync()
+                t3 = time.perf_counter()
+                cl = res["cloud"]
+                n = cl.total()
+                P, C = cl.xyz[:n].cpu().numpy(), cl.bgr[:n].cpu().numpy()
+                t4 = time.perf_counter()
+                ply.save_ply(P, C, os.path.join(f, os.path.basename(f) + ".ply"))
+                t5 = time.perf_counter()
+                for k, (x, y) in zip(st, ((t0, t1), (t1, t2), (t2, t3), (t3, t4), (t4, t5))):
+                    st[k].append(1e3 * (y - x))
+                pts.append(n)
+                del ds, dt, res, cl, P, C, stack, texture
+            ply_bytes = os.path.getsize(os.path.join(folders[-1], os.path.basename(folders[-1]) + ".ply"))
+            gc_ms = []
+            for f in folders:
+                t0 = time.perf_counter()
+                with contextlib.redirect_stdout(_io.StringIO()):
+                    slsys.generate_cloud(f, calib_file)
+                gc_ms.append(1e3 * (time.perf_counter() - t0))
+            med = {k: statistics.median(v) for k, v in st.items()}
+            limiting = max(med, key=med.get)
+            print(json.dumps({"leg": "gui_stages", "format": fmt, "views": a.views, "H": a.H, "W": a.W,
+                              "files_per_view": 46, "bytes_on_disk_per_view": disk,
+                              "stage_ms_median": med, "stage_ms_all": st, "limiting_stage": limiting,
+                              "sum_of_stages_ms": sum(med.values()),
+                              "generate_cloud_ms_median": statistics.median(gc_ms), "generate_cloud_ms": gc_ms,
+                              "views_per_s_gui": 1e3 / statistics.median(gc_ms),
+                              "points_per_view": int(statistics.median(pts)), "ply_bytes_per_view": ply_bytes,
+                              "folders_write_s": write_s,
+                              "note": "page cache warm; decode_files = io.read_stack (46 files + colour file 0, "
+                                      "8 threads); kernels = decode_triangulate + sync (f64 xyz); ply = native "
+                                      "%.4f ASCII writer, 16 threads"}), flush=True)
+            # ---- batch: generate_clouds, pipelined ----
+            for f in folders:
+                os.remove(os.path.join(f, os.path.basename(f) + ".ply"))
+            with contextlib.redirect_stdout(_io.StringIO()):
+                slsys.generate_clouds(folders[:2], calib_file)  # warm: pools, pinned slots
+            t0 = time.perf_counter()
+            with contextlib.redirect_stdout(_io.StringIO()):
+                slsys.generate_clouds(folders, calib_file)
+            el = time.perf_counter() - t0
+            # the pipeline's stages in isolation, per view: 24 planes decoded into one buffer, the PLY
+            files = io.list_stack_files(folders[0])
+            buf = np.empty((24, a.H, a.W), np.uint8)
+            tex = np.empty((a.H, a.W, 3), np.uint8)
+            fills = []
+            for f in folders:
+                t1 = time.perf_counter()
+                io.fill_stack(io.list_stack_files(f), buf, tex)
+                fills.append(1e3 * (time.perf_counter() - t1))
+            print(json.dumps({"leg": "batch", "format": fmt, "views": a.views, "wall_s": el,
+                              "views_per_s": a.views / el, "px_per_s": a.views * px / el,
+                              "fill_24_planes_ms_median": statistics.median(fills),
+                              "ply_ms_median": med["ply"], "kernels_ms_median": med["kernels"],
+                              "limiting_stage": "decode_files" if statistics.median(fills) > med["ply"] else "ply",
+                              "note": "SLSystem.generate_clouds (ViewPipeline, 3 slots: decode of the 24 cloud "
+                                      "planes, H2D, kernels, D2H, PLY overlapped); stage costs in isolation beside"}),
+                  flush=True)
+            shutil.rmtree(fdir, ignore_errors=True)
+            del files
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+        pool.shutdown()
+
+
+if __name__ == "__main__":
+    main()

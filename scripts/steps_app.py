@@ -66,6 +66,7 @@ for i in range(a.steps):
     s_, t_, o_ = slots[i % len(slots)]
     nxt = slots[(i + S) % len(slots)][0] if a.next_stats else None
     pool.decode_triangulate(s_, 1920, 1080, texture=t_, maps=not a.cloud_only, cloud=True, xyz_dtype=torch.float32,
-                            out=o_, next_stack=nxt, poses=poses, wait_inputs=False, lane=i % S)
+                            out=o_, next_stack=nxt, poses=poses, wait_inputs=False, lane=i % S,
+                            prepared=True)
 pool.sync()
 print(f"steps {a.steps} ring {R} lanes {S} points {int(slots[0][2]['view_offsets'][-1].item())}")

@@ -579,19 +579,25 @@ class ReconstructorPool:
             e.reserve(max_views, max_px)
 
     def decode_triangulate(self, stack: torch.Tensor, n_cols: int = 1920, n_rows: int = 1080, *,
-                           wait_inputs: bool = True, lane: int | None = None, **kw):
+                           wait_inputs: bool = True, lane: int | None = None, prepared: bool = False, **kw):
         """``Reconstructor.decode_triangulate`` on the next lane (same
         arguments; ``stream`` is the lane's own and ``out`` the lane's buffers
         when the pool reuses outputs).  ``wait_inputs=False`` skips the wait
         on the caller's stream and the allocator bookkeeping for inputs the
-        caller knows are ready and kept alive (e.g. resident stacks).
+        caller knows are ready and kept alive (e.g. resident stacks); with the
+        pool's own reused outputs such calls are prepared once per lane and
+        argument set (sl_call_prepare) and re-run with one C call.
         ``lane``: run on that lane (the round-robin continues after it)
         instead of the next one.  ``next_stack``: the stack of THIS LANE's
-        next call, as Reconstructor.decode_triangulate's.  With
-        ``wait_inputs=False`` an explicit ``out`` dict (the caller's buffers
-        for this argument set, e.g. one per resident view) takes the prepared
-        path too; the caller then also guarantees that no other lane writes
-        those buffers meanwhile."""
+        next call, as Reconstructor.decode_triangulate's.  ``prepared=True``
+        (with ``wait_inputs=False``) lets an explicit ``out`` dict -- the
+        caller's buffers for this argument set, e.g. one per resident view --
+        take the prepared path as well: the lane then keeps that dict and its
+        buffers bound to a prepared call (at most 8 per lane, the least
+        recently used one released first; an ``out`` dict bound to another
+        argument set is re-bound), and the caller guarantees that no other
+        lane writes those buffers meanwhile.  Without it an explicit ``out``
+        runs the plain call: nothing is kept."""
         if "stream" in kw:
             raise ValueError("ReconstructorPool picks the stream (one per lane)")
         if lane is not None and not 0 <= lane < len(self.engines):
@@ -605,8 +611,9 @@ class ReconstructorPool:
             for t in (stack, kw.get("texture"), kw.get("poses")):
                 if isinstance(t, torch.Tensor) and t.is_cuda:
                     t.record_stream(st)  # the caller may free it before the lane has read it
-        outs = kw.get("out") if kw.get("out") is not None else self._outs[i]
-        if not wait_inputs and outs is not None and \
+        explicit = kw.get("out") is not None
+        outs = kw.get("out") if explicit else self._outs[i]
+        if not wait_inputs and outs is not None and (prepared or not explicit) and \
                 kw.get("mask_counts") is None and not kw.get("stack_ready"):
             nxt = kw.pop("next_stack", None)
             kw.pop("out", None)
@@ -617,17 +624,21 @@ class ReconstructorPool:
                     None if pos is None else pos.data_ptr(), kw.get("maps", False), kw.get("cloud", True),
                     kw.get("xyz_dtype", torch.float32), kw.get("fast_f32", False), kw.get("mask_mode", "adaptive"),
                     id(outs))
-            plans = self._plans[i]
-            ent = plans.get(pkey)  # (the outputs dict, held: its id stays unique) + the prepared call
+            plans = self._plans[i]  # insertion order = recency (moved to the end on use)
+            ent = plans.pop(pkey, None)  # (the outputs dict, held: its id stays unique) + the prepared call
             if ent is None:
-                if len(plans) >= 8:  # a bounded set of resident argument sets per lane
-                    for _, q in plans.values():
-                        q.close()
-                    plans.clear()
+                # prepare() re-points the dict's entries: a plan of another
+                # argument set bound to the same dict would write buffers the
+                # dict no longer names, so it is released first
+                for k in [k for k, (o, _) in plans.items() if o is outs]:
+                    plans.pop(k)[1].close()
+                while len(plans) >= 8:  # a bounded set of resident argument sets per lane: release the LRU one
+                    plans.pop(next(iter(plans)))[1].close()
                 pk = {k: v for k, v in kw.items() if k not in ("mask_counts", "stack_ready")}
                 with torch.cuda.stream(st):  # outputs (re)allocated here belong to the lane stream
-                    ent = plans[pkey] = (outs, eng.prepare(stack, n_cols, n_rows, out=outs, **pk))
+                    ent = (outs, eng.prepare(stack, n_cols, n_rows, out=outs, **pk))
                 self._keys[i] = None
+            plans[pkey] = ent
             res = dict(ent[1].run(st, next_stack=nxt))
             res["stream"] = st
             res["lane"] = i

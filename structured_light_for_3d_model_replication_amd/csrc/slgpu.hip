@@ -26,13 +26,16 @@
 // Frames that do not fit it (unaligned, W or H > 4096, Wp > 2048) run
 // k_decode (codes + histogram) -> k_count (mask, decision) -> k_cloud.
 //
-// Scratch is clean at every launch-group boundary, whatever ran before: the
-// kernel that consumes an accumulated buffer (k_decode / k_count the
-// histograms, k_cloud the super-block sums) zeroes it once its last reader is
-// done (a per-buffer arrival counter), so a captured hipGraph replays in any
-// phase.  The one thing that crosses a boundary is a pre-stats pass queued for
-// the next call, which the host hands on only within one capture (or eager
-// call sequence).
+// Scratch at a launch-group boundary never depends on the host's view of the
+// sequence, so a captured hipGraph replays in any phase: the histograms are
+// zeroed by their last reader (k_decode / k_count, a per-view arrival
+// counter); the super-block sums alternate between two buffers selected on
+// the device -- the producer (k_decode / k_count) accumulates into the buffer
+// selector word par[0] names and zeroes the other one (super_produce), the
+// consumer (k_cloud) only flips the selector (super_consume), so the buffer it
+// read keeps its sums until the next producer zeroes it.  The one thing that
+// crosses a boundary is a pre-stats pass queued for the next call, which the
+// host hands on only within one capture (or eager call sequence).
 //
 // Everything in this file is compiled with -ffp-contract=off.
 #include <hip/hip_runtime.h>
@@ -2474,15 +2477,17 @@ int capture_of(sl_ctx* c, hipStream_t s, unsigned long long* out) {
 // bits.  Launch groups hold at most kMaxChunks chunks (at least one view); a
 // group's points follow the earlier groups' (base_in).
 //
-// Scratch at every launch-group boundary: the super-block buffer is zero (its
-// consumer, k_cloud, zeroes it) and so is the histogram buffer (k_decode /
-// k_count zero what they read), except that it may hold one queued pre-stats
-// pass for the next group or call.  A call takes a queued pass only when it
-// is of its first group's stack, stride, views and frame AND was queued in
-// the same stream capture (or both eagerly): a captured graph never depends
-// on a pass queued outside it, so it replays in any phase, any number of
-// times.  A pass not taken is cleared (a memset on the stream) before the
-// buffer is used again; so is anything a failed call left behind.
+// Scratch at every launch-group boundary: the super-block buffer the next
+// producer accumulates into is zeroed by that producer itself (super_produce:
+// the two buffers alternate on the device, k_cloud only flips the selector),
+// and the histogram buffer is zero (k_decode / k_count zero what they read)
+// except that it may hold one queued pre-stats pass for the next group or
+// call.  A call takes a queued pass only when it is of its first group's
+// stack, stride, views and frame AND was queued in the same stream capture
+// (or both eagerly): a captured graph never depends on a pass queued outside
+// it, so it replays in any phase, any number of times.  A pass not taken is
+// cleared (k_zero on the stream) before the buffer is used again; so is
+// anything a failed call left behind.
 int launch_groups(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int count_mode, int cloud_mode,
                   hipStream_t s, PreArms arms) {
   const bool decide = (decode_mode & M_DECIDE) != 0;
@@ -3351,8 +3356,19 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
   if (!c->last.valid) return fail(c, SL_EINVAL, "sl_time_kernels: no earlier call to re-run");
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->last.s;
+  // Measurement only, and eager only: it waits on its events, and its clears
+  // are hipMemsetAsync (a memset node captured into a graph is what round 5
+  // saw fill with a wrong byte on replays).  Refused while the
+  // stream is capturing.
+  {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    HIP_TRY(c, hipStreamIsCapturing(s, &st));
+    if (st != hipStreamCaptureStatusNone)
+      return fail(c, SL_EINVAL, "sl_time_kernels: the last call's stream is capturing (re-runs are eager only)");
+  }
   // The launch consumed its inputs (its k_decode / k_count zeroed the
-  // histograms they read, its k_cloud the super-block sums): from clean
+  // histograms they read; the super-block sums it accumulated are stale
+  // until the next producer zeroes them): from clean
   // scratch they are rebuilt once, untimed, then every kernel re-runs with
   // `rerun` set (consumers leave their inputs as they are).  k_cloud first --
   // it reads the super-block sums the producers' re-runs add into again --

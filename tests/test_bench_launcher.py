@@ -44,6 +44,8 @@ def test_gpus_n_starts_n_ranks(n, scaling, views, expect):
     assert len(m["per_rank_s"]) == n and all(s >= 0 for s in m["per_rank_s"])
     assert m["per_rank_points"] == m["gather_counts"] == r["counts"]
     assert m["gather_bytes_to_root"] == 15 * (expect - r["counts"][0])
+    # what the gather must move, stated before it runs
+    assert m["bytes_per_point"] == 15 and m["expected_gather_bytes_to_root"] == m["gather_bytes_to_root"]
     assert m["gather_ms"] > 0 and m["gather_GBps"] > 0
     # the strong-scaled config-3 leg (36 views sharded over the N ranks)
     sc = m["strong_c3"]
@@ -53,6 +55,10 @@ def test_gpus_n_starts_n_ranks(n, scaling, views, expect):
     assert sc["gather_counts"] == [1000 * v for v in sc["per_rank_views"]] == sc["per_rank_points"]
     assert len(sc["per_rank_ms_per_step"]) == n and sc["ms_per_step"] == max(sc["per_rank_ms_per_step"])
     assert sc["px_per_s"] > 0 and sc["gather_bytes_to_root"] == 15 * 1000 * (36 - sc["per_rank_views"][0])
+    assert sc["expected_gather_bytes_to_root"] == sc["gather_bytes_to_root"]
+    # the shard imbalance's bound on strong-scaling efficiency: 36 / (N x max views)
+    assert sc["ideal_strong_efficiency"] == pytest.approx(36 / (n * max(sc["per_rank_views"])))
+    assert sc["ideal_strong_efficiency"] == pytest.approx({2: 1.0, 3: 1.0}[n])
 
 
 def test_gpus_disagreeing_with_world_size_is_an_error():
@@ -73,6 +79,10 @@ def test_streams_defaults_per_config():
     # c2: two lanes over a ring of distinct resident views (round 5: 2 lanes
     # 114 vs 121 us per step once the maps and xyz left with nt stores)
     assert bench.CONFIGS["c2"]["streams"] == 2 and bench.CONFIGS["c2"]["ring"] == 3
+    # c1's control window: distinct views whose inputs exceed the 256 MiB Infinity Cache
+    c1 = bench.CONFIGS["c1"]
+    assert c1["ring_control"] * c1["H"] * c1["W"] * (2 + 2 * 10 + 3) > 2 ** 28
+    assert c1["ring_control"] % c1["streams"] == 0 and bench.parse([]).ring_control is None
 
 
 def test_headline_is_the_reference_arithmetic():
@@ -106,14 +116,14 @@ def test_bench_defaults_next_stats_and_graph():
 
 
 def test_committed_traffic_profiles_match_the_configs():
-    """bench.py attaches profiles/r05_traffic2/traffic_<config>.json to a line
-    only when the profile's workload is the line's (config, views per GPU,
+    """bench.py attaches <bench.TRAFFIC_DIR>/traffic_<config>.json (the
+    directory bench.py itself reads by default) to a line only when the profile's workload is the line's (config, views per GPU,
     decide path, exact xyz): every config of the bench but c1 has one that
     matches, with calibrated per-kernel bytes that add up."""
     sys.path.insert(0, REPO)
     import bench
     for name in ("c2", "c3", "c4", "c5"):
-        path = os.path.join(REPO, "profiles", "r05_traffic2", f"traffic_{name}.json")
+        path = os.path.join(REPO, bench.TRAFFIC_DIR, f"traffic_{name}.json")
         tj = json.load(open(path))
         assert tj["config"] == name and tj["views"] == bench.CONFIGS[name]["views"], name
         assert tj["decide"] is True and tj["xyz"] == "exact" and tj["calibration"], name
@@ -123,3 +133,11 @@ def test_committed_traffic_profiles_match_the_configs():
         S = c.get("streams", 1)
         want_ring = S * -(-c["ring"] // S) if "ring" in c else 1  # bench.py: the ring rounded up to the lanes
         assert tj.get("ring", 1) == want_ring, name
+
+
+def test_ideal_strong_efficiency_of_the_c3_shards():
+    """VERDICT r5 #6: the 8-GPU strong leg is capped by its 5-vs-4-view shards."""
+    sys.path.insert(0, REPO)
+    import bench
+    assert bench.ideal_strong_efficiency(36, 8) == pytest.approx(0.9)
+    assert [bench.ideal_strong_efficiency(36, n) for n in (1, 2, 3, 4)] == [1.0, 1.0, 1.0, 1.0]

@@ -216,7 +216,7 @@ def test_pool_view_ring_explicit_outputs():
         v = i % 4
         assert pool._next == i % 2  # round-robin
         res[v] = pool.decode_triangulate(views[v][0], 1920, 1080, texture=views[v][1], maps=True, cloud=True,
-                                         xyz_dtype=torch.float32, wait_inputs=False, out=outs[v],
+                                         xyz_dtype=torch.float32, wait_inputs=False, out=outs[v], prepared=True,
                                          next_stack=views[(v + 2) % 4][0])
         assert res[v]["lane"] == v % 2
     pool.sync()
@@ -259,7 +259,8 @@ def test_pool_lanes_captured_in_one_graph():
     def step(i):
         v = i % 4
         res[v] = pool.decode_triangulate(views[v][0], 1920, 1080, texture=views[v][1], maps=True, cloud=True,
-                                         wait_inputs=False, out=outs[v], next_stack=views[(v + 2) % 4][0],
+                                         wait_inputs=False, out=outs[v], prepared=True,
+                                         next_stack=views[(v + 2) % 4][0],
                                          lane=i % 2)
 
     cur = torch.cuda.Stream()
@@ -286,3 +287,58 @@ def test_pool_lanes_captured_in_one_graph():
                     np.testing.assert_array_equal(a, b)
     del g
     pool.close()
+
+
+def test_pool_explicit_out_is_not_kept_unless_prepared():
+    """an explicit ``out`` with wait_inputs=False runs the plain
+    call unless the caller opts in (``prepared=True``): a fresh ``out={}`` per
+    call keeps no prepared call and no outputs alive (device memory flat over
+    20 calls).  Opted in: at most 8 prepared calls per lane, the least
+    recently used released first; an ``out`` dict re-bound to another
+    argument set releases its old plan; every result equal to the engine's."""
+    from structured_light_for_3d_model_replication_amd import core, synth
+    rig = synth.Rig(H=96, W=160, Wp=256, Hp=128)
+    calib = synth.make_calibration(rig, with_Nc=False)
+    views = _views(10, rig, synth)
+    eng = core.Reconstructor(torch.device("cuda", 0))
+    eng.set_calibration(calib, rig.H, rig.W)
+    want = []
+    for s, t in views:
+        r = eng.decode_triangulate(s, rig.Wp, rig.Hp, texture=t, maps=True, cloud=True)
+        eng.sync()
+        want.append(_host(r))
+    pool = core.ReconstructorPool(torch.device("cuda", 0), lanes=1)
+    pool.set_calibration(calib, rig.H, rig.W)
+    kw = dict(maps=True, cloud=True, wait_inputs=False)
+    mem = []
+    for k in range(20):
+        s, t = views[k % 10]
+        r = pool.decode_triangulate(s, rig.Wp, rig.Hp, texture=t, out={}, **kw)
+        pool.sync()
+        for a, b in zip(_host(r), want[k % 10]):
+            np.testing.assert_array_equal(a, b)
+        del r
+        assert len(pool._plans[0]) == 0
+        mem.append(torch.cuda.memory_allocated())
+    assert mem[-1] == mem[9], mem  # flat: nothing kept per call
+    # opted in: one plan per (argument set, dict), LRU-bounded at 8
+    outs = [{} for _ in views]
+    for k in range(10):
+        s, t = views[k]
+        r = pool.decode_triangulate(s, rig.Wp, rig.Hp, texture=t, out=outs[k], prepared=True, **kw)
+        pool.sync()
+        for a, b in zip(_host(r), want[k]):
+            np.testing.assert_array_equal(a, b)
+    plans = pool._plans[0]
+    assert len(plans) == 8
+    assert {id(o) for o, _ in plans.values()} == {id(o) for o in outs[2:]}  # views 0 and 1 released
+    # re-use view 2's plan (now the most recent), then bind view 2's dict to view 0's arguments
+    pool.decode_triangulate(views[2][0], rig.Wp, rig.Hp, texture=views[2][1], out=outs[2], prepared=True, **kw)
+    assert id(list(plans.values())[-1][0]) == id(outs[2])
+    r = pool.decode_triangulate(views[0][0], rig.Wp, rig.Hp, texture=views[0][1], out=outs[2], prepared=True, **kw)
+    pool.sync()
+    assert sum(o is outs[2] for o, _ in plans.values()) == 1 and len(plans) == 8
+    for a, b in zip(_host(r), want[0]):
+        np.testing.assert_array_equal(a, b)
+    pool.close()
+    eng.close()
