@@ -45,6 +45,8 @@ def main():
             bad += nz != 0
             print(json.dumps({"variant": "torch_graph_keep" if keep else "torch_graph_destroyed", "replay": r,
                               "capture_rc": rc, "nonzero_words": nz, "word0": f"0x{first & 0xffffffff:08x}",
+                              # the garbage against the device addresses the graph's nodes hold
+                              "h_ptr": f"0x{h.data_ptr():x}", "res_ptr": f"0x{res.data_ptr():x}",
                               "ok": nz == 0}), flush=True)
         del g
     print(json.dumps({"torch": torch.__version__, "hip": torch.version.hip, "bad_replays": bad}), flush=True)

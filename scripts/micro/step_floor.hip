@@ -33,7 +33,10 @@
 // Variants: full | no_pre (no pre-stats reads) | no_rec (no records written /
 // read) | bare (neither) | decode (f_decode only) | cloud (f_cloud only) |
 // lanes1 (one lane) | chain (each decode after the previous call's decode:
-// decode beside cloud) | mix (one linear kernel per step reading and writing the
+// decode beside cloud) | fulla (full, the point stores in windows aligned to
+// 128-B lines of the output) | cloud1 / cloud1a (f_cloud alone, one lane, no
+// pre-stats: k_cloud's re-run; unaligned / aligned store windows) |
+// mix (one linear kernel per step reading and writing the
 // step's bytes in 16-B grid-stride streams: the chip's rate for this
 // read/write mix in its most favourable form).
 // One JSON line per (variant, rep): µs per step, bytes, TB/s.
@@ -87,6 +90,7 @@ struct P {
   int64_t pre_vs;
   int pre_views, pre_bpv;
   unsigned* sink;
+  int align;              // store windows aligned to 128-B lines of the output (xyz: 32 points, BGR: 128)
 };
 
 template <int READ>
@@ -202,11 +206,15 @@ __global__ __launch_bounds__(kThreads, 5) void f_cloud(P p) {
   const int64_t base = static_cast<int64_t>(view) * p.out_vs + static_cast<int64_t>(civ) * n;  // 4 | base
   float* const wx = p.xyz + 3 * base;
   uint8_t* const wc = p.bgr + 3 * base;
-  for (int k = lane; k < n / 4; k += 64) {
+  const int sh_c = p.align ? static_cast<int>((base & 127) >> 2) : 0;  // quads before the first 128-point boundary
+  const int sh_x = p.align ? static_cast<int>(base & 31) : 0;          // points before the first 32-point boundary
+  for (int k = lane - sh_c; k < n / 4; k += 64) {
+    if (k < 0) continue;
     const uint32_t* s = &s_bgr[wid][(3 * 4 * k) / 4 % (3 * kChunk / 4)];
     *reinterpret_cast<v3u*>(wc + 12 * k) = v3u{s[0], s[1], s[2]};
   }
-  for (int j = lane; j < n; j += 64) {
+  for (int j = lane - sh_x; j < n; j += 64) {
+    if (j < 0) continue;
     const unsigned f = static_cast<unsigned>(j) ^ s_bgr[wid][j % (3 * kChunk / 4)];
     float* q = wx + 3 * j;
     __builtin_nontemporal_store(__uint_as_float(f), q);
@@ -341,7 +349,7 @@ int main(int argc, char** argv) {
   // of beside its decode (the read-heavy / write-heavy pairing)
   std::vector<hipEvent_t> dec_done(lanes);
   for (int l = 0; l < lanes; ++l) CHECK(hipEventCreateWithFlags(&dec_done[l], hipEventDisableTiming));
-  bool chain = false;
+  bool chain = false, align = false;
   auto enqueue_call = [&](int step, int lanes_used, bool pre, bool rec, bool dec, bool cld) {
     const int l = step % lanes_used, r = step % ring;
     const int r_next = (step + lanes_used) % ring;  // this lane's next call's slot
@@ -370,6 +378,7 @@ int main(int argc, char** argv) {
       p.bgr = o.bgr + 3 * out_vs * v0;
       p.sink = sink;
       p.cloud_gx = ngroups;
+      p.align = align ? 1 : 0;
       // the pass of the next group of this call, or of the lane's next call's first group
       const bool last = v0 + group >= views;
       const uint8_t* pst = last ? st[r_next] : st[r] + (v0 + group) * stack_vs;
@@ -412,11 +421,13 @@ int main(int argc, char** argv) {
   };
 
   auto run = [&](const std::string& var) -> double {
-    const bool pre = var != "no_pre" && var != "bare" && var != "mix";
+    const bool pre = var != "no_pre" && var != "bare" && var != "mix" && var != "cloud1" && var != "cloud1a";
     const bool rec = var != "no_rec" && var != "bare";
-    const bool dec = var != "cloud", cld = var != "decode";
+    const bool dec = var != "cloud" && var != "cloud1" && var != "cloud1a",
+               cld = var != "decode";
     chain = var == "chain";
-    const int L = var == "lanes1" ? 1 : lanes;
+    align = var == "fulla" || var == "cloud1a";
+    const int L = (var == "lanes1" || var == "cloud1" || var == "cloud1a") ? 1 : lanes;
     auto one = [&](int i) {
       if (var == "mix") enqueue_mix(i, L);
       else enqueue_call(i, L, pre, rec, dec, cld);
@@ -453,19 +464,21 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < reps; ++rep) {
     for (const auto& var : vars) {
       const double us = run(var);
-      const bool pre = var != "no_pre" && var != "bare" && var != "mix";
+      const bool c1v = var == "cloud1" || var == "cloud1a";
+      const bool pre = var != "no_pre" && var != "bare" && var != "mix" && !c1v;
       const bool rec = var != "no_rec" && var != "bare";
       double moved = 0.0;
       if (var == "mix") moved = 16.0 * (mix_rd16 + mix_wr16);
       else {
-        if (var != "cloud") moved += b_stack + b_maps + (rec ? b_rec : 0.0);
+        if (var != "cloud" && !c1v) moved += b_stack + b_maps + (rec ? b_rec : 0.0);
         if (var != "decode") moved += b_tex + b_pts + (rec ? b_rec : 0.0) + (pre ? b_pre : 0.0);
       }
       printf("{\"variant\": \"%s\", \"rep\": %d, \"H\": %d, \"W\": %d, \"planes_read\": %d, \"maps\": %d, "
              "\"views_per_call\": %d, \"group\": %d, \"ring\": %d, \"lanes\": %d, \"points_per_view\": %lld, "
              "\"steps\": %d, \"us_per_step\": %.2f, \"algorithmic_MB\": %.1f, \"moved_MB\": %.1f, "
              "\"algorithmic_TBps\": %.3f, \"moved_TBps\": %.3f, \"frac_of_8TBps\": %.4f}\n",
-             var.c_str(), rep, H, W, rd, maps, views, group, ring, var == "lanes1" ? 1 : lanes,
+             var.c_str(), rep, H, W, rd, maps, views, group, ring,
+             (var == "lanes1" || var == "cloud1" || var == "cloud1a") ? 1 : lanes,
              static_cast<long long>(out_vs), steps, us, algo / 1e6, moved / 1e6, algo / us / 1e6, moved / us / 1e6,
              algo / us / 1e6 / 8.0);
       fflush(stdout);

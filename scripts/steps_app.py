@@ -6,7 +6,7 @@ divides every step kernel's summed bytes by N (the first call's k_stats,
 which no earlier call computed, is 1/N of a k_stats per step).
 
     python scripts/steps_app.py [--steps 40] [--no-next-stats] [--ring R] [--lanes S] [--views V --cloud-only]
-                                [--config c3|c4|c5]
+                                [--config c1|c3|c4|c5]
 
 --ring R (config 2, default 3 as bench.py): the steps cycle through R distinct
 resident views (own stack, texture and outputs; R rounded up to a multiple of
@@ -36,19 +36,23 @@ ap.add_argument("--poses", action="store_true", help="turntable poses (config 5'
 ap.add_argument("--ring", type=int, default=3, help="config 2: distinct resident views cycled (bench.py --ring)")
 ap.add_argument("--lanes", type=int, default=2, help="views in flight (bench.py --streams)")
 ap.add_argument("--config", default=None,
-                help="c3 / c4 / c5: that bench config's call (frame, views, cloud only, pose) instead")
+                help="c1 / c3 / c4 / c5: that bench config's call (frame, views, cloud only, pose) instead "
+         "(c1: one 1280x720 view, 1024-column projector, 22 planes, maps + cloud)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
-H, W, deg = 2160, 3840, 1.0
-if a.config:  # bench.py CONFIGS: one call = the config's views of one GPU
+H, W, deg, Wp, Hp, rows = 2160, 3840, 1.0, 1920, 1080, True
+if a.config == "c1":  # bench.py CONFIGS["c1"]: one view, maps + cloud, the chain over one resident view
+    H, W, Wp, Hp, rows, a.ring = 720, 1280, 1024, 768, False, 1
+elif a.config:  # bench.py CONFIGS: one call = the config's views of one GPU
     H, W, a.views, deg = {"c3": (1080, 1920, 36, 10.0), "c4": (3000, 4000, 45, 1.0), "c5": (2160, 3840, 45, 1.0)}[a.config]
     a.cloud_only, a.poses = True, a.config == "c5"
-rig = synth.Rig(H=H, W=W)
+rig = synth.Rig(H=H, W=W, Wp=Wp, Hp=Hp)
 cal = synth.make_calibration(rig, with_Nc=False)
 S = max(1, a.lanes)
-R = S * -(-max(1, a.ring) // S) if a.views == 1 and not a.config else 1
-ring = [synth.render_stack(rig, seed=3000 + k, view_deg=7.0 * k, device=dev) for k in range(1, R)]
-views = [synth.render_stack(rig, seed=2000 + v, view_deg=deg * v, device=dev) for v in range(a.views)]
+R = S * -(-max(1, a.ring) // S) if a.views == 1 and a.config in (None, "c1") and a.ring > 1 else 1
+ring = [synth.render_stack(rig, seed=3000 + k, view_deg=7.0 * k, include_rows=rows, device=dev) for k in range(1, R)]
+views = [synth.render_stack(rig, seed=2000 + v, view_deg=deg * v, include_rows=rows, device=dev)
+         for v in range(a.views)]
 st = torch.stack([s_ for s_, _ in views]) if a.views > 1 else views[0][0]
 tx = torch.stack([t_ for _, t_ in views]) if a.views > 1 else views[0][1]
 del views
@@ -65,7 +69,7 @@ torch.cuda.synchronize(dev)
 for i in range(a.steps):
     s_, t_, o_ = slots[i % len(slots)]
     nxt = slots[(i + S) % len(slots)][0] if a.next_stats else None
-    pool.decode_triangulate(s_, 1920, 1080, texture=t_, maps=not a.cloud_only, cloud=True, xyz_dtype=torch.float32,
+    pool.decode_triangulate(s_, Wp, Hp, texture=t_, maps=not a.cloud_only, cloud=True, xyz_dtype=torch.float32,
                             out=o_, next_stack=nxt, poses=poses, wait_inputs=False, lane=i % S,
                             prepared=True)
 pool.sync()

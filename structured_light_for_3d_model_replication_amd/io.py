@@ -16,9 +16,13 @@ OpenCV is not available in this image, so the other decoding uses Pillow.  For
 single-channel files (what the fixtures and the synthetic rig produce) gray is
 the identity and colour is the channel replicated three times, exactly what
 cv2 returns.  Colour files are converted with OpenCV's fixed-point BT.601
-weights ``(1868 B + 9617 G + 4899 R + 8192) >> 14``.  JPEG payloads saved under a
-.bmp name (server/server.py:70) decode through Pillow's libjpeg, whose output
-is not pinned against OpenCV's: parity for such captures is unpinned.
+weights ``(1868 B + 9617 G + 4899 R + 8192) >> 14``.  JPEG payloads (also the
+ones saved under a .bmp name, server/server.py:70) are read as gray the way
+cv2.imread(f, 0) reads them: libjpeg asked for grayscale output, i.e. the
+decoded luma (Y) channel (Pillow's ``draft("L")``), with no colour
+conversion -- 2-3x faster than decoding RGB and converting.  Pillow's libjpeg
+is not pinned against OpenCV's (no cv2 here): parity for such captures is
+unpinned.
 """
 from __future__ import annotations
 
@@ -123,6 +127,10 @@ def imread_gray(path: str, out: np.ndarray | None = None) -> np.ndarray:
     if a is not None:
         return a
     with Image.open(path) as im:
+        if im.format == "JPEG" and im.mode in ("RGB", "YCbCr"):
+            # OpenCV's JPEG decoder with IMREAD_GRAYSCALE sets libjpeg's
+            # out_color_space = JCS_GRAYSCALE: the luma plane as decoded
+            im.draft("L", im.size)
         if im.mode == "L":
             return np.asarray(im).copy()
         if im.mode in ("I;16", "I", "F"):
@@ -149,6 +157,17 @@ _POOLS: dict = {}
 _POOL_LOCK = threading.Lock()
 
 
+def default_workers() -> int:
+    """Decoding threads: the process's core share (OMP_NUM_THREADS, which the
+    GPU box sets to its 16-core share; os.cpu_count() there is the whole
+    machine's), at most 16.  Pillow's PNG and JPEG decoders release the GIL:
+    16 threads decode a 4K view's 24 PNG files in 91 ms against 121 ms with 8
+    (profiles/r02_ingest_mi355x_box.jsonl)."""
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    n = int(share) if share.isdigit() and int(share) > 0 else (os.cpu_count() or 1)
+    return max(1, min(16, n))
+
+
 def _pool(workers: int):
     """A persistent pool of exactly ``workers`` decoding threads."""
     from concurrent.futures import ThreadPoolExecutor
@@ -158,13 +177,14 @@ def _pool(workers: int):
         return _POOLS[workers]
 
 
-def fill_stack(files: list[str], stack_out, tex_out, workers: int = 8) -> bool:
+def fill_stack(files: list[str], stack_out, tex_out, workers: int | None = None) -> bool:
     """Decode files[0 : len(stack_out)] as gray straight into ``stack_out``
     (uint8 [n, H, W], e.g. a pinned tensor's numpy view) and file 0 in colour
     into ``tex_out`` [H, W, 3] BGR -- unless file 0 is single-channel, whose
     colour read is the gray plane replicated (cv2.imread): then ``tex_out`` is
     left untouched and True is returned (the caller may pass no texture)."""
     n = len(stack_out)
+    workers = default_workers() if workers is None else workers
     if len(files) < n:
         raise ValueError(f"{len(files)} files for {n} planes")
     shape = tuple(stack_out.shape[1:])
@@ -189,8 +209,9 @@ def fill_stack(files: list[str], stack_out, tex_out, workers: int = 8) -> bool:
     return gray
 
 
-def read_stack(folder: str, workers: int = 8):
+def read_stack(folder: str, workers: int | None = None):
     """-> (stack uint8 [n_img, H, W], texture uint8 [H, W, 3] BGR, files)."""
+    workers = default_workers() if workers is None else workers
     files = list_stack_files(folder)
     if len(files) < 4:
         raise ValueError("Not enough images in folder to decode.")

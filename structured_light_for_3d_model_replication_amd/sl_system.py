@@ -20,12 +20,13 @@ methods of the reference class are outside this package's scope.
 from __future__ import annotations
 
 import os
+import threading
 
 import numpy as np
 import scipy.io
 import torch
 
-from . import core, io, ply
+from . import core, io, pipeline, ply
 
 
 def _to_numpy_calib(data) -> dict:
@@ -68,22 +69,51 @@ def reconstruct_point_cloud(col_map, row_map, mask, texture, calib, *, device=No
     return cloud.xyz[:n].cpu().numpy().astype(np.float64, copy=False), cloud.bgr[:n].cpu().numpy()
 
 
+_STAGE = {}  # (device, n_up, H, W) -> the one-view path's pinned host and device stack / texture buffers
+_STAGE_LOCK = threading.Lock()
+
+
+def _stage(dev, n_up, H, W):
+    key = (str(dev), n_up, H, W)
+    if key not in _STAGE:
+        if len(_STAGE) >= 2:  # a frame-size change releases the older buffers
+            _STAGE.pop(next(iter(_STAGE)))
+        _STAGE[key] = (torch.empty((n_up, H, W), dtype=torch.uint8, pin_memory=True),
+                       torch.empty((H, W, 3), dtype=torch.uint8, pin_memory=True),
+                       torch.empty((n_up, H, W), dtype=torch.uint8, device=dev),
+                       torch.empty((H, W, 3), dtype=torch.uint8, device=dev))
+    return _STAGE[key]
+
+
 def decode_and_reconstruct(folder, calib, n_cols=1920, n_rows=1080, *, mask_mode="adaptive", device=None,
-                           xyz_dtype=np.float64, count_valid=False):
+                           xyz_dtype=np.float64, count_valid=False, prepared=None):
     """gray_decode + reconstruct_point_cloud fused in one GPU pass (what
-    generate_cloud runs).  Row planes are not read: the cloud uses only the
-    column code (sl_system.py:624-629).  ``count_valid``: also return the
-    number of masked-in pixels (the kernels count them: sl_mask_counts_to)."""
-    stack, texture, _ = io.read_stack(folder)
+    generate_cloud runs).  The whole file list is checked with gray_decode's
+    rules (sl_system.py:515-516, 549-554: ValueError below 4 files,
+    IndexError for a pattern without its inverse), but only the files the
+    cloud reads are decoded -- white, black and the column pairs (24 of 46 for
+    11 + 11 bits): reconstruct_point_cloud uses only col_map (:624-629) -- into
+    pinned buffers kept for the next call, and uploaded from there.
+    ``count_valid``: also return the number of masked-in pixels (the kernels
+    count them: sl_mask_counts_to).  ``prepared``: calibration_key(calib, H,
+    W) when the caller has it (SLSystem.generate_cloud caches it per file)."""
+    files = io.list_stack_files(folder)
+    n_up = pipeline.planes_for_cloud(len(files), n_cols, n_rows)
+    H, W = io.frame_size(files[0])
     eng = core.engine(device)
-    H, W = stack.shape[1:]
-    eng.set_calibration(calib, H, W)
+    eng.set_calibration(calib, H, W, _prepared=prepared)
     tdt = torch.float64 if np.dtype(xyz_dtype) == np.float64 else torch.float32
     mc = torch.empty(1, dtype=torch.int64, device=eng.device) if count_valid else None
-    res = eng.decode_triangulate(torch.from_numpy(stack).to(eng.device), n_cols, n_rows,
-                                 texture=torch.from_numpy(texture).to(eng.device), mask_mode=mask_mode,
-                                 maps=False, cloud=True, xyz_dtype=tdt, mask_counts=mc)
-    eng.sync()
+    with _STAGE_LOCK:  # the staging buffers are shared by the calls of this process
+        hs, ht, ds, dt = _stage(eng.device, n_up, H, W)
+        gray_tex = io.fill_stack(files, hs.numpy(), ht.numpy())
+        s = torch.cuda.current_stream(eng.device)
+        ds.copy_(hs, non_blocking=True)
+        if not gray_tex:
+            dt.copy_(ht, non_blocking=True)
+        res = eng.decode_triangulate(ds, n_cols, n_rows, texture=None if gray_tex else dt, mask_mode=mask_mode,
+                                     maps=False, cloud=True, xyz_dtype=tdt, mask_counts=mc, stream=s)
+        eng.sync(s)
     cloud = res["cloud"]
     n = cloud.total()
     P, C = cloud.xyz[:n].cpu().numpy().astype(np.float64, copy=False), cloud.bgr[:n].cpu().numpy()
@@ -107,6 +137,10 @@ def index_error_stage(n_files: int, n_cols: int = 1920, n_rows: int = 1080):
     return None
 
 
+_CALIB = {}  # calib file identity -> (calib dict, {(H, W): calibration_key}); see SLSystem._calib
+_CALIB_LOCK = threading.Lock()
+
+
 class SLSystem:
     """Reconstruction part of server/sl_system.py:14 ``SLSystem``."""
 
@@ -120,10 +154,7 @@ class SLSystem:
         if not os.path.exists(calib_file):
             raise FileNotFoundError(f"Calibration file not found at {calib_file}")
         print(f"[Process] Processing {scan_dir} using {calib_file}...")
-        data = scipy.io.loadmat(calib_file)
-        if "Oc" not in data:
-            raise ValueError("Calibration file missing 'Oc'.")
-        calib = _to_numpy_calib(data)
+        calib, keys = self._calib(calib_file)
         # gray_decode's checks and prints, in the reference's order (:510-516,
         # :549-554, :574-577): the stack's faults raise where it would
         n_files = len(io.list_stack_files(scan_dir))
@@ -137,12 +168,42 @@ class SLSystem:
         if stage == "rows":
             raise IndexError("list index out of range")
         print("Reconstructing 3D points...")
-        points, colors, n_valid = decode_and_reconstruct(scan_dir, calib, device=self.device, count_valid=True)
+        files = io.list_stack_files(scan_dir)
+        hw = io.frame_size(files[0])
+        with _CALIB_LOCK:
+            if hw not in keys:  # the content key (and pinhole check) of this calibration at this frame size
+                keys[hw] = core.Reconstructor.calibration_key(calib, *hw)
+            prepared = keys[hw]
+        points, colors, n_valid = decode_and_reconstruct(scan_dir, calib, device=self.device, count_valid=True,
+                                                         prepared=prepared)
         print(f"Processing {n_valid} valid pixels...")
         out_path = os.path.join(scan_dir, os.path.basename(scan_dir) + ".ply")
         print(f"Saving {len(points)} points to {out_path}...")
         ply.save_ply(points, colors, out_path)
         print(f"[Success] Generated {out_path}")
+
+    @staticmethod
+    def _calib(calib_file):
+        """calib.mat loaded as generate_cloud loads it (sl_system.py:496-504:
+        scipy.io.loadmat, the 'Oc' check, the five arrays), kept while the
+        file is the same (path, inode, size, mtime): a GUI session decodes
+        many scans with one calibration, and a 4K calib.mat's Nc table takes
+        ~0.2 s to load and as long again to key."""
+        st = os.stat(calib_file)
+        ident = (os.path.realpath(calib_file), st.st_ino, st.st_size, st.st_mtime_ns)
+        with _CALIB_LOCK:
+            hit = _CALIB.get(ident)
+        if hit is not None:
+            return hit
+        data = scipy.io.loadmat(calib_file)
+        if "Oc" not in data:
+            raise ValueError("Calibration file missing 'Oc'.")
+        hit = (_to_numpy_calib(data), {})
+        with _CALIB_LOCK:
+            for k in [k for k in _CALIB if k[0] == ident[0]]:
+                del _CALIB[k]  # an older version of this file
+            _CALIB[ident] = hit
+        return hit
 
     def generate_clouds(self, scan_dirs, calib_file, *, slots=3):
         """Batched ``generate_cloud``: every folder of ``scan_dirs``
