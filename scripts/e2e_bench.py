@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import argparse
 import contextlib
+import ctypes
 import io as _io
 import json
 import os
@@ -46,7 +47,7 @@ import torch
 from PIL import Image
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from structured_light_for_3d_model_replication_amd import core, io, pipeline, ply, sl_system, synth  # noqa: E402
+from structured_light_for_3d_model_replication_amd import _lib, core, io, pipeline, ply, sl_system, synth  # noqa: E402
 
 
 def write_folder(folder, stack, fmt, pool):
@@ -100,6 +101,7 @@ def main():
             # page cache warm for every leg (the files were just written)
             # ---- gui_stages: generate_cloud's work, stage by stage ----
             st = {k: [] for k in ("decode_files", "h2d", "kernels", "d2h", "ply")}
+            fmt_ms = []
             pts = []
             eng.set_calibration(cal, a.H, a.W)
             for f in folders:
@@ -124,6 +126,10 @@ def main():
                 t4 = time.perf_counter()
                 ply.save_ply(P, C, os.path.join(f, os.path.basename(f) + ".ply"))
                 t5 = time.perf_counter()
+                ln = ctypes.c_int64()  # the formatting alone (sl_format_ply's size query formats every line)
+                _lib.check(_lib.load().sl_format_ply(P.ctypes.data, _lib.SL_XYZ_F64, C.ctypes.data, len(P), ply._THREADS,
+                                                     None, 0, ctypes.byref(ln)), None, "sl_format_ply")
+                fmt_ms.append(1e3 * (time.perf_counter() - t5))
                 for k, (x, y) in zip(st, ((t0, t1), (t1, t2), (t2, t3), (t3, t4), (t4, t5))):
                     st[k].append(1e3 * (y - x))
                 pts.append(n)
@@ -156,6 +162,7 @@ def main():
             print(json.dumps({"leg": "gui_stages", "format": fmt, "views": a.views, "H": a.H, "W": a.W,
                               "files_per_view": 46, "bytes_on_disk_per_view": disk,
                               "stage_ms_median": med, "stage_ms_all": st, "limiting_stage": limiting,
+                              "ply_format_only_ms_median": statistics.median(fmt_ms),
                               "sum_of_stages_ms": sum(med.values()),
                               "generate_cloud_ms_median": statistics.median(gc_ms), "generate_cloud_ms": gc_ms,
                               "views_per_s_gui": 1e3 / statistics.median(gc_ms),

@@ -2451,10 +2451,16 @@ PreArms take_arms(sl_ctx* c) {
   return a;
 }
 
-// Zero n words at p on stream s.  A kernel, not hipMemsetAsync: captured into
-// a hipGraph, a memset node of the histogram buffer left garbage in it from
-// the graph's second replay on (measured: scripts/dbg/graph1b.py; the kernel
-// and no clear at all both replay bit-exactly).
+// Zero n words at p on stream s.  A kernel, not hipMemsetAsync: inside a
+// torch process this library runs on torch's bundled HIP runtime (7.0.51831,
+// loaded first under the soname libamdhip64.so.7), whose captured memset
+// nodes fill their buffer, from a graph's third launch on, with the low 32
+// bits of another node's pointer argument instead of their value
+// (scripts/dbg/graph_memset_torch.py: every word = low half of the next
+// kernel's output address; profiles/r06_memset/).  The same
+// graphs on ROCm 7.2's runtime replay clean (scripts/dbg/graph_memset.hip).
+// Round 5 saw exactly that in the adaptive mask's max word (thresholds 0 /
+// -7.4e8).  Kernel nodes are not affected.
 __global__ __launch_bounds__(256) void k_zero(unsigned* p, int64_t n) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += 256ll * gridDim.x) p[i] = 0u;
 }
@@ -3406,9 +3412,8 @@ int sl_time_kernels(sl_ctx* c, int reps, double* decode_ms, double* count_ms, do
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->last.s;
   // Measurement only, and eager only: it waits on its events, and its clears
-  // are hipMemsetAsync (a memset node captured into a graph is what round 5
-  // saw fill with a wrong byte on replays).  Refused while the
-  // stream is capturing.
+  // are hipMemsetAsync, which torch's bundled HIP runtime mis-replays as
+  // graph nodes (k_zero).  Refused while the stream is capturing.
   {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     HIP_TRY(c, hipStreamIsCapturing(s, &st));

@@ -167,7 +167,9 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
 
         def fill(i, stack, tex, group=group):
             try:
-                return io.fill_stack(files[group[i]], stack.numpy(), tex.numpy())
+                # half the core share: the D2H thread formats the previous views' PLY files meanwhile
+                return io.fill_stack(files[group[i]], stack.numpy(), tex.numpy(),
+                                     workers=max(1, io.default_workers() // 2))
             except (OSError, ValueError) as e:
                 if raise_errors:
                     raise
