@@ -56,7 +56,7 @@ from structured_light_for_3d_model_replication_amd import core, parallel, synth 
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # the committed calibrated-PMC traffic profiles the lines cite (scripts/gpu_r4_traffic.sh)
-TRAFFIC_DIR = os.path.join("profiles", "r05_traffic3")
+TRAFFIC_DIR = os.path.join("profiles", "r06_traffic")
 
 CONFIGS = {
     # BASELINE.json configs.  views = views per GPU per step (weak scaling;
