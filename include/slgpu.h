@@ -251,6 +251,16 @@ int sl_format_ply(const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n,
 /* Write that text to `path` (replaces save_ply, sl_system.py:665-691). */
 int sl_write_ply(const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n, int threads);
 
+/* The same file from a cloud in device memory (xyz / bgr device pointers,
+ * e.g. a call's outputs): the text is formatted on the device (one thread
+ * per point, the host formatter's digit code) into context scratch, copied
+ * back through a pinned buffer in chunks and written, the host formatting
+ * nothing; byte-identical to sl_write_ply.  A cloud with a non-finite
+ * coordinate or |x| >= 9e11 (printed through libc's %.4f) is copied back and
+ * formatted on the host instead.  Blocking on `stream` (hipStream_t). */
+int sl_write_ply_device(sl_ctx* ctx, const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n,
+                        void* stream);
+
 /* Binary little-endian PLY with the same header properties (float x y z,
  * uchar red green blue; colour swapped from BGR): 15-byte records, xyz rounded
  * to float32 when xyz_dtype is SL_XYZ_F64.  A compact binary form of the

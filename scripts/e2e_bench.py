@@ -100,8 +100,8 @@ def main():
             disk = sum(os.path.getsize(os.path.join(folders[0], x)) for x in os.listdir(folders[0]))
             # page cache warm for every leg (the files were just written)
             # ---- gui_stages: generate_cloud's work, stage by stage ----
-            st = {k: [] for k in ("decode_files", "h2d", "kernels", "d2h", "ply")}
-            fmt_ms = []
+            st = {k: [] for k in ("decode_files", "h2d", "kernels", "ply")}
+            host_ply = {k: [] for k in ("d2h", "ply_host", "format_only")}
             pts = []
             eng.set_calibration(cal, a.H, a.W)
             for f in folders:
@@ -122,16 +122,24 @@ def main():
                 t3 = time.perf_counter()
                 cl = res["cloud"]
                 n = cl.total()
-                P, C = cl.xyz[:n].cpu().numpy(), cl.bgr[:n].cpu().numpy()
+                path = os.path.join(f, os.path.basename(f) + ".ply")
+                ply.save_ply_device(cl.xyz[:n], cl.bgr[:n], path)  # generate_cloud's PLY: formatted on the GPU
                 t4 = time.perf_counter()
-                ply.save_ply(P, C, os.path.join(f, os.path.basename(f) + ".ply"))
+                for k, (x, y) in zip(st, ((t0, t1), (t1, t2), (t2, t3), (t3, t4))):
+                    st[k].append(1e3 * (y - x))
+                # beside it, the host formatter's route: D2H of the points, format + write on 16 threads
+                os.remove(path)
                 t5 = time.perf_counter()
+                P, C = cl.xyz[:n].cpu().numpy(), cl.bgr[:n].cpu().numpy()
+                t6 = time.perf_counter()
+                ply.save_ply(P, C, path)
+                t7 = time.perf_counter()
                 ln = ctypes.c_int64()  # the formatting alone (sl_format_ply's size query formats every line)
                 _lib.check(_lib.load().sl_format_ply(P.ctypes.data, _lib.SL_XYZ_F64, C.ctypes.data, len(P), ply._THREADS,
                                                      None, 0, ctypes.byref(ln)), None, "sl_format_ply")
-                fmt_ms.append(1e3 * (time.perf_counter() - t5))
-                for k, (x, y) in zip(st, ((t0, t1), (t1, t2), (t2, t3), (t3, t4), (t4, t5))):
-                    st[k].append(1e3 * (y - x))
+                t8 = time.perf_counter()
+                for k, (x, y) in zip(host_ply, ((t5, t6), (t6, t7), (t7, t8))):
+                    host_ply[k].append(1e3 * (y - x))
                 pts.append(n)
                 del res, cl, P, C
             ply_bytes = os.path.getsize(os.path.join(folders[-1], os.path.basename(folders[-1]) + ".ply"))
@@ -162,7 +170,7 @@ def main():
             print(json.dumps({"leg": "gui_stages", "format": fmt, "views": a.views, "H": a.H, "W": a.W,
                               "files_per_view": 46, "bytes_on_disk_per_view": disk,
                               "stage_ms_median": med, "stage_ms_all": st, "limiting_stage": limiting,
-                              "ply_format_only_ms_median": statistics.median(fmt_ms),
+                              "host_ply_route_ms_median": {k: statistics.median(v) for k, v in host_ply.items()},
                               "sum_of_stages_ms": sum(med.values()),
                               "generate_cloud_ms_median": statistics.median(gc_ms), "generate_cloud_ms": gc_ms,
                               "views_per_s_gui": 1e3 / statistics.median(gc_ms),
@@ -170,8 +178,10 @@ def main():
                               "folders_write_s": write_s, "generate_cloud_profile_cum_ms": profile_top,
                               "note": "page cache warm; decode_files = the 24 cloud files into pinned staging "
                                       "(io.fill_stack, 8 threads; the colour re-read of file 0 when it is not "
-                                      "single-channel); kernels = decode_triangulate + sync (f64 xyz); ply = "
-                                      "native %.4f ASCII writer, 16 threads; generate_cloud_ms[0] includes the "
+                                      "single-channel); kernels = decode_triangulate + sync (f64 xyz); ply = the "
+                                      "text formatted on the GPU, copied back in chunks, written (generate_cloud's "
+                                      "route); host_ply_route = D2H of the points + the host formatter on 16 "
+                                      "threads (+ its formatting alone); generate_cloud_ms[0] includes the "
                                       "calib.mat load + key (a 3 x H*W Nc table)"}), flush=True)
             # ---- batch: generate_clouds, pipelined ----
             for f in folders:

@@ -33,7 +33,7 @@ SL_XYZ_F32_FAST = 2
 EXPORTS = ("sl_abi_version", "sl_ctx_create", "sl_ctx_destroy", "sl_ctx_last_error", "sl_ctx_reserve",
            "sl_set_calib", "sl_decode_triangulate", "sl_mask_counts_to", "sl_stack_ready", "sl_stack_next", "sl_call_prepare", "sl_call_run", "sl_call_destroy", "sl_triangulate_maps", "sl_sync",
            "sl_last_thresholds", "sl_last_launch_info", "sl_profile_enable", "sl_profile_read", "sl_time_kernels", "sl_format_ply", "sl_write_ply",
-           "sl_write_ply_binary", "sl_voxel_downsample", "sl_statistical_outliers", "sl_select_by_index",
+           "sl_write_ply_device", "sl_write_ply_binary", "sl_voxel_downsample", "sl_statistical_outliers", "sl_select_by_index",
            "sl_transform_points", "sl_estimate_normals", "sl_icp_point_to_plane", "sl_radius_search", "sl_compute_fpfh",
            "sl_feature_nn", "sl_ransac_feature_matching", "sl_merge_pool_trim", "sl_calib_products", "sl_gather_unique_id", "sl_gather_init", "sl_gather_counts",
            "sl_gather",
@@ -71,6 +71,7 @@ _SIGS = {
                                 ctypes.POINTER(ctypes.c_double)]),
     "sl_format_ply": (_i32, [_vp, _i32, _vp, _i64, _i32, _vp, _i64, ctypes.POINTER(_i64)]),
     "sl_write_ply": (_i32, [ctypes.c_char_p, _vp, _i32, _vp, _i64, _i32]),
+    "sl_write_ply_device": (_i32, [_vp, ctypes.c_char_p, _vp, _i32, _vp, _i64, _vp]),
     "sl_write_ply_binary": (_i32, [ctypes.c_char_p, _vp, _i32, _vp, _i64, _i32]),
     "sl_voxel_downsample": (_i32, [_vp, _vp, _vp, _i64, ctypes.c_double, _vp, _vp, ctypes.POINTER(_i64), _vp]),
     "sl_statistical_outliers": (_i32, [_vp, _vp, _i64, _i32, ctypes.c_double, _vp, _vp, ctypes.POINTER(_i64), _vp]),

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import hashlib
+import os
 import threading
 import weakref
 from dataclasses import dataclass
@@ -429,6 +430,25 @@ class Reconstructor:
                                          counts, int(root), _ptr(xo) if total else None,
                                          _ptr(bo) if total else None, st), self._ctx, "sl_gather")
         return xo, bo, list(counts)
+
+    def write_ply(self, path, xyz: torch.Tensor, bgr: torch.Tensor, stream=None) -> None:
+        """The reference's ASCII PLY (sl_system.py:665-691) of a cloud in this
+        device's memory, formatted on the GPU (sl_write_ply_device): ``xyz``
+        (n, 3) float32 / float64, ``bgr`` (n, 3) uint8, both contiguous on this
+        device.  Byte-identical to ``ply.save_ply`` of the same points.
+        Blocking: the file is written when this returns."""
+        if xyz.device != self.device or bgr.device != self.device:
+            raise ValueError("write_ply: xyz and bgr must be on this Reconstructor's device")
+        if xyz.dtype not in (torch.float32, torch.float64) or bgr.dtype != torch.uint8:
+            raise TypeError("write_ply: xyz float32 / float64, bgr uint8")
+        if xyz.dim() != 2 or xyz.shape[1] != 3 or tuple(bgr.shape) != tuple(xyz.shape):
+            raise ValueError("write_ply: xyz and bgr must both be (n, 3)")
+        xyz, bgr = xyz.contiguous(), bgr.contiguous()
+        dt = _lib.SL_XYZ_F64 if xyz.dtype == torch.float64 else _lib.SL_XYZ_F32
+        with self._lock:
+            _lib.check(self._L.sl_write_ply_device(self._ctx, os.fsencode(path), xyz.data_ptr(), dt, bgr.data_ptr(),
+                                                   xyz.shape[0], self._stream(stream)), self._ctx,
+                       f"cannot write {path}")
 
     def sync(self, stream=None) -> None:
         """Wait for this context's work and raise on device-side failures."""

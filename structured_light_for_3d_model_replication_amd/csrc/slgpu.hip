@@ -2237,6 +2237,16 @@ struct sl_ctx {
   void* comm = nullptr;
   int nranks = 0, rank = 0;
   int64_t* d_gcounts = nullptr;
+  // sl_write_ply_device: per-workgroup line bytes and offsets, the text, and
+  // the pinned host buffer it comes back through (grown, kept)
+  unsigned* d_ply_bsum = nullptr;
+  int64_t cap_ply_bsum = 0;
+  int64_t* d_ply_boff = nullptr;
+  int64_t cap_ply_boff = 0;
+  char* d_ply_text = nullptr;
+  int64_t cap_ply_text = 0;
+  char* h_ply_text = nullptr;
+  int64_t cap_h_ply_text = 0;
   int64_t cap_gcounts = 0;
   // the last call's stream: a call on another stream first waits for the work
   // queued there (the scratch above is per context)
@@ -2764,20 +2774,21 @@ int slgpu_device(const sl_ctx* c) { return c->device; }
 // computed exactly in 128-bit integers from x's binary significand, printed
 // with 4 decimals.  Values beyond 2^53 / 10^4 and non-finite ones go through
 // glibc's snprintf("%.4f"), which is also correctly rounded ("nan", "inf"
-// as Python prints them).
+// as Python prints them).  The digit code is shared by the host formatter and
+// the device one (k_ply_*, sl_write_ply_device): one source, the same bytes.
 namespace {
 
-char* fmt4(char* o, double x) {
-  uint64_t bits;
-  memcpy(&bits, &x, 8);
-  const bool neg = bits >> 63;
+// finite and |x| < 9e11: the exact integer path applies (else libc, host only)
+__host__ __device__ inline bool fmt4_exact(double x) {
+  return __builtin_isfinite(x) && __builtin_fabs(x) < 9.0e11;
+}
+
+// round(|x| * 10^4), ties to even, exactly (fmt4_exact(x) holds); *neg: the sign bit
+__host__ __device__ inline uint64_t fmt4_scaled(double x, bool* neg) {
+  const uint64_t bits = static_cast<uint64_t>(__builtin_bit_cast(int64_t, x));
+  *neg = bits >> 63;
   const int be = static_cast<int>((bits >> 52) & 0x7ff);
   const uint64_t frac = bits & ((1ull << 52) - 1);
-  if (be == 0x7ff || fabs(x) >= 9.0e11) {  // non-finite or large: libc
-    if (be == 0x7ff && frac) return o + sprintf(o, "nan");
-    if (be == 0x7ff) return o + sprintf(o, neg ? "-inf" : "inf");
-    return o + sprintf(o, "%.4f", x);
-  }
   // x = m * 2^e exactly
   const uint64_t m = be ? (frac | (1ull << 52)) : frac;
   const int e = (be ? be : 1) - 1075;
@@ -2795,12 +2806,31 @@ char* fmt4(char* o, double x) {
     N = static_cast<uint64_t>(q);
     if (r > half || (r == half && (N & 1u))) ++N;  // round half to even
   }
+  return N;
+}
+
+// the length of fmt4_digits' text for x
+__host__ __device__ inline int fmt4_len(double x) {
+  bool neg;
+  uint64_t ip = fmt4_scaled(x, &neg) / 10000u;
+  int d = 1;
+  while (ip >= 10u) {
+    ip /= 10u;
+    ++d;
+  }
+  return (neg ? 1 : 0) + d + 5;
+}
+
+// x with 4 decimals, correctly rounded (fmt4_exact(x) holds); -> end of text
+__host__ __device__ inline char* fmt4_digits(char* o, double x) {
+  bool neg;
+  const uint64_t N = fmt4_scaled(x, &neg);
   if (neg) *o++ = '-';
-  // the digits of ip = N / 10^4, then 4 decimals, two at a time from a table
-  static constexpr char kPairs[201] =
-      "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
-      "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
-      "8081828384858687888990919293949596979899";
+  // the digits of ip = N / 10^4, then 4 decimals, two at a time
+  auto pair = [](unsigned r, char* d) {
+    d[0] = static_cast<char>('0' + r / 10u);
+    d[1] = static_cast<char>('0' + r % 10u);
+  };
   const uint64_t ip = N / 10000u;
   const unsigned fp = static_cast<unsigned>(N - ip * 10000u);
   char t[24];
@@ -2809,23 +2839,60 @@ char* fmt4(char* o, double x) {
   while (a >= 100u) {
     const unsigned r = static_cast<unsigned>(a % 100u);
     a /= 100u;
-    t[k++] = kPairs[2 * r + 1];
-    t[k++] = kPairs[2 * r];
+    char d[2];
+    pair(r, d);
+    t[k++] = d[1];
+    t[k++] = d[0];
   }
   if (a >= 10u) {
-    t[k++] = kPairs[2 * a + 1];
-    t[k++] = kPairs[2 * a];
+    char d[2];
+    pair(static_cast<unsigned>(a), d);
+    t[k++] = d[1];
+    t[k++] = d[0];
   } else {
     t[k++] = static_cast<char>('0' + a);
   }
   while (k) *o++ = t[--k];
   *o++ = '.';
-  const unsigned hi = fp / 100u, lo = fp - hi * 100u;
-  o[0] = kPairs[2 * hi];
-  o[1] = kPairs[2 * hi + 1];
-  o[2] = kPairs[2 * lo];
-  o[3] = kPairs[2 * lo + 1];
+  pair(fp / 100u, o);
+  pair(fp % 100u, o + 2);
   return o + 4;
+}
+
+char* fmt4(char* o, double x) {
+  if (!fmt4_exact(x)) {  // non-finite or large: libc
+    if (x != x) return o + sprintf(o, "nan");
+    if (__builtin_isinf(x)) return o + sprintf(o, x < 0 ? "-inf" : "inf");
+    return o + sprintf(o, "%.4f", x);
+  }
+  return fmt4_digits(o, x);
+}
+
+__host__ __device__ inline int u8_len(unsigned v) { return v >= 100 ? 3 : v >= 10 ? 2 : 1; }
+
+__host__ __device__ inline char* fmt_u8_hd(char* o, unsigned v) {
+  if (v >= 100) *o++ = static_cast<char>('0' + v / 100u);
+  if (v >= 10) *o++ = static_cast<char>('0' + v / 10u % 10u);
+  *o++ = static_cast<char>('0' + v % 10u);
+  return o;
+}
+
+// one point's line "x y z r g b\n" (every coordinate fmt4_exact) -> end
+__host__ __device__ inline char* ply_line(char* o, double x, double y, double z, unsigned b, unsigned g,
+                                          unsigned r) {
+  o = fmt4_digits(o, x);
+  *o++ = ' ';
+  o = fmt4_digits(o, y);
+  *o++ = ' ';
+  o = fmt4_digits(o, z);
+  *o++ = ' ';
+  o = fmt_u8_hd(o, r);
+  *o++ = ' ';
+  o = fmt_u8_hd(o, g);
+  *o++ = ' ';
+  o = fmt_u8_hd(o, b);
+  *o++ = '\n';
+  return o;
 }
 
 char* fmt_u8(char* o, unsigned v) {
@@ -2837,6 +2904,119 @@ char* fmt_u8(char* o, unsigned v) {
 
 bool ply_args_ok(const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n) {
   return n >= 0 && (n == 0 || (xyz && bgr)) && (xyz_dtype == SL_XYZ_F32 || xyz_dtype == SL_XYZ_F64);
+}
+
+// ---- the same text on the device (sl_write_ply_device) ----
+// One thread per point, kPlyBlock points per workgroup.  k_ply_len: every
+// line's length from the exact scaled values (no text), summed per workgroup;
+// a coordinate outside fmt4_exact sets *fallback (libc's %.4f: the host
+// formats that cloud).  k_ply_scan: one workgroup turns the sums into each
+// workgroup's byte offset (+ the total at [nb]).  k_ply_text: every line
+// written into LDS at its offset inside the workgroup's span, then the span
+// to global memory, 256 consecutive bytes per store round.
+constexpr int kPlyBlock = 256;
+constexpr int kPlyLineMax = 72;  // longest line with every |coordinate| < 9e11: 3 x 18 + 3 + 11 + 1 = 69
+
+template <typename T>
+__device__ inline void ply_point(const T* xyz, const uint8_t* bgr, int64_t i, double* v, unsigned* c) {
+  v[0] = static_cast<double>(xyz[3 * i]);
+  v[1] = static_cast<double>(xyz[3 * i + 1]);
+  v[2] = static_cast<double>(xyz[3 * i + 2]);
+  c[0] = bgr[3 * i];
+  c[1] = bgr[3 * i + 1];
+  c[2] = bgr[3 * i + 2];
+}
+
+template <typename T>
+__device__ inline unsigned ply_line_len(const T* xyz, const uint8_t* bgr, int64_t i, int64_t n, bool* bad) {
+  *bad = false;
+  if (i >= n) return 0u;
+  double v[3];
+  unsigned c[3];
+  ply_point(xyz, bgr, i, v, c);
+  if (!(fmt4_exact(v[0]) && fmt4_exact(v[1]) && fmt4_exact(v[2]))) {
+    *bad = true;
+    return 0u;
+  }
+  return static_cast<unsigned>(fmt4_len(v[0]) + fmt4_len(v[1]) + fmt4_len(v[2]) + u8_len(c[0]) + u8_len(c[1]) +
+                               u8_len(c[2]) + 6);
+}
+
+// inclusive scan over the workgroup (kPlyBlock threads); *total: the sum
+__device__ inline unsigned ply_block_scan(unsigned x, unsigned* s_w, unsigned* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned t = __shfl_up(x, d, 64);
+    if (lane >= d) x += t;
+  }
+  if (lane == 63) s_w[wid] = x;
+  __syncthreads();
+  unsigned before = 0u, all = 0u;
+#pragma unroll
+  for (int w = 0; w < kPlyBlock / 64; ++w) {
+    before += w < wid ? s_w[w] : 0u;
+    all += s_w[w];
+  }
+  *total = all;
+  return x + before;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kPlyBlock) void k_ply_len(const T* xyz, const uint8_t* bgr, int64_t n, unsigned* bsum,
+                                                        unsigned* fallback) {
+  __shared__ unsigned s_w[kPlyBlock / 64];
+  bool bad;
+  const unsigned len = ply_line_len(xyz, bgr, static_cast<int64_t>(blockIdx.x) * kPlyBlock + threadIdx.x, n, &bad);
+  if (bad) atomicOr(fallback, 1u);
+  unsigned total;
+  (void)ply_block_scan(len, s_w, &total);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void k_ply_scan(const unsigned* bsum, int64_t nb, int64_t* boff) {
+  __shared__ long long s_w[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t per = (nb + 1023) / 1024, lo = tid * per, hi = std::min<int64_t>(nb, lo + per);
+  long long mine = 0;
+  for (int64_t b = lo; b < hi; ++b) mine += bsum[b];
+  long long x = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const long long t = __shfl_up(x, d, 64);
+    if (lane >= d) x += t;
+  }
+  if (lane == 63) s_w[wid] = x;
+  __syncthreads();
+  long long before = 0;
+  for (int w = 0; w < wid; ++w) before += s_w[w];
+  long long off = x - mine + before;  // exclusive
+  for (int64_t b = lo; b < hi; ++b) {
+    boff[b] = off;
+    off += bsum[b];
+  }
+  if (tid == 1023) boff[nb] = off;  // the text's total bytes
+}
+
+template <typename T>
+__global__ __launch_bounds__(kPlyBlock) void k_ply_text(const T* xyz, const uint8_t* bgr, int64_t n,
+                                                         const int64_t* boff, char* out) {
+  __shared__ unsigned s_w[kPlyBlock / 64];
+  __shared__ char s_txt[kPlyBlock * kPlyLineMax];
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kPlyBlock + threadIdx.x;
+  bool bad;
+  const unsigned len = ply_line_len(xyz, bgr, i, n, &bad);
+  unsigned total;
+  const unsigned end = ply_block_scan(len, s_w, &total);
+  if (len) {
+    double v[3];
+    unsigned c[3];
+    ply_point(xyz, bgr, i, v, c);
+    (void)ply_line(s_txt + (end - len), v[0], v[1], v[2], c[0], c[1], c[2]);
+  }
+  __syncthreads();
+  char* dst = out + boff[blockIdx.x];
+  for (unsigned j = threadIdx.x; j < total; j += kPlyBlock) dst[j] = s_txt[j];
 }
 
 // Header + the point lines in `threads` contiguous parts (formatted in
@@ -2952,6 +3132,10 @@ void sl_ctx_destroy(sl_ctx* c) {
     if (Rccl* R = rccl()) (void)R->comm_destroy(static_cast<ncclComm_t>(c->comm));
   }
   if (c->d_gcounts) (void)hipFree(c->d_gcounts);
+  for (void* ptr : {static_cast<void*>(c->d_ply_bsum), static_cast<void*>(c->d_ply_boff),
+                    static_cast<void*>(c->d_ply_text)})
+    if (ptr) (void)hipFree(ptr);
+  if (c->h_ply_text) (void)hipHostFree(c->h_ply_text);
   if (c->done_ev) (void)hipEventDestroy(c->done_ev);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (void* ptr : {static_cast<void*>(c->d_planes), static_cast<void*>(c->d_xn), static_cast<void*>(c->d_yn),
@@ -3579,6 +3763,112 @@ int sl_write_ply(const char* path, const void* xyz, int xyz_dtype, const uint8_t
   for (size_t t = 0; ok && t < parts.len.size(); ++t) ok = put(parts.ptr[t], parts.len[t]);
   ok = (close(fd) == 0) && ok;
   return ok ? SL_OK : SL_EIO;
+}
+
+// The cloud a call left in HBM, formatted on the device and written: the
+// lines' lengths and offsets, the text into device scratch, then back in
+// chunks through a pinned buffer, each chunk written while the next one is
+// in flight.  A cloud with a coordinate the exact path does not take (non-
+// finite, |x| >= 9e11) is copied back and formatted on the host instead.
+int sl_write_ply_device(sl_ctx* c, const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n,
+                        void* stream) {
+  if (!c || !path || !ply_args_ok(xyz, xyz_dtype, bgr, n)) return SL_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t nb = std::max<int64_t>(1, (n + kPlyBlock - 1) / kPlyBlock);
+  int r = grow(c, &c->d_ply_bsum, &c->cap_ply_bsum, nb + 1);  // [nb]: the fallback flag
+  if (r) return r;
+  r = grow(c, &c->d_ply_boff, &c->cap_ply_boff, nb + 1);
+  if (r) return r;
+  unsigned* flag = c->d_ply_bsum + nb;
+  r = zero_async(c, flag, 1, s);
+  if (r) return r;
+  const bool f64 = xyz_dtype == SL_XYZ_F64;
+  if (n > 0) {
+    if (f64)
+      hipLaunchKernelGGL(k_ply_len<double>, dim3(static_cast<unsigned>(nb)), dim3(kPlyBlock), 0, s,
+                         static_cast<const double*>(xyz), bgr, n, c->d_ply_bsum, flag);
+    else
+      hipLaunchKernelGGL(k_ply_len<float>, dim3(static_cast<unsigned>(nb)), dim3(kPlyBlock), 0, s,
+                         static_cast<const float*>(xyz), bgr, n, c->d_ply_bsum, flag);
+    hipLaunchKernelGGL(k_ply_scan, dim3(1), dim3(1024), 0, s, c->d_ply_bsum, nb, c->d_ply_boff);
+    HIP_TRY(c, hipGetLastError());
+  }
+  int64_t total = 0;
+  unsigned fallback = 0;
+  if (n > 0) {
+    HIP_TRY(c, hipMemcpyAsync(&total, c->d_ply_boff + nb, sizeof(total), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(&fallback, flag, sizeof(fallback), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  if (fallback) {  // libc's %.4f for some coordinate: the host formatter on a host copy
+    const size_t esz = f64 ? 8 : 4;
+    std::vector<char> hx(static_cast<size_t>(n) * 3 * esz);
+    std::vector<uint8_t> hb(static_cast<size_t>(n) * 3);
+    HIP_TRY(c, hipMemcpyAsync(hx.data(), xyz, hx.size(), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(hb.data(), bgr, hb.size(), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    return sl_write_ply(path, hx.data(), xyz_dtype, hb.data(), n, 16);
+  }
+  r = grow(c, &c->d_ply_text, &c->cap_ply_text, std::max<int64_t>(total, 1));
+  if (r) return r;
+  if (n > 0) {
+    if (f64)
+      hipLaunchKernelGGL(k_ply_text<double>, dim3(static_cast<unsigned>(nb)), dim3(kPlyBlock), 0, s,
+                         static_cast<const double*>(xyz), bgr, n, c->d_ply_boff, c->d_ply_text);
+    else
+      hipLaunchKernelGGL(k_ply_text<float>, dim3(static_cast<unsigned>(nb)), dim3(kPlyBlock), 0, s,
+                         static_cast<const float*>(xyz), bgr, n, c->d_ply_boff, c->d_ply_text);
+    HIP_TRY(c, hipGetLastError());
+  }
+  if (total > c->cap_h_ply_text) {
+    if (c->h_ply_text) HIP_TRY(c, hipHostFree(c->h_ply_text));
+    c->h_ply_text = nullptr;
+    c->cap_h_ply_text = 0;
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_ply_text), static_cast<size_t>(total)));
+    c->cap_h_ply_text = total;
+  }
+  char hb[256];
+  const int hl = snprintf(hb, sizeof(hb),
+                          "ply\nformat ascii 1.0\nelement vertex %lld\nproperty float x\nproperty float y\n"
+                          "property float z\nproperty uchar red\nproperty uchar green\nproperty uchar blue\n"
+                          "end_header\n",
+                          static_cast<long long>(n));
+  // the text back in chunks (events on the stream), each written as it lands
+  constexpr int64_t kChunkBytes = int64_t{32} << 20;
+  const int nch = static_cast<int>(std::max<int64_t>(1, (total + kChunkBytes - 1) / kChunkBytes));
+  std::vector<hipEvent_t> evs(nch, nullptr);
+  bool ok = true;
+  for (int k = 0; k < nch && ok; ++k) {
+    const int64_t lo = k * kChunkBytes, len = std::min(total, lo + kChunkBytes) - lo;
+    ok = hipEventCreateWithFlags(&evs[k], hipEventDisableTiming) == hipSuccess &&
+         (len <= 0 || hipMemcpyAsync(c->h_ply_text + lo, c->d_ply_text + lo, static_cast<size_t>(len),
+                                     hipMemcpyDeviceToHost, s) == hipSuccess) &&
+         hipEventRecord(evs[k], s) == hipSuccess;
+  }
+  const int fd = ok ? open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0666) : -1;
+  auto put = [fd](const char* p, size_t len) -> bool {
+    while (len) {
+      const ssize_t w = write(fd, p, len);
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) return false;
+      p += w;
+      len -= static_cast<size_t>(w);
+    }
+    return true;
+  };
+  bool io_ok = fd >= 0 && put(hb, static_cast<size_t>(hl));
+  for (int k = 0; k < nch; ++k) {
+    const int64_t lo = k * kChunkBytes, len = std::min(total, lo + kChunkBytes) - lo;
+    const bool landed = evs[k] && hipEventSynchronize(evs[k]) == hipSuccess;
+    ok = ok && landed;
+    if (io_ok && landed && len > 0) io_ok = put(c->h_ply_text + lo, static_cast<size_t>(len));
+  }
+  for (hipEvent_t e : evs)
+    if (e) (void)hipEventDestroy(e);
+  if (fd >= 0) io_ok = (close(fd) == 0) && io_ok;
+  if (!ok) return fail(c, SL_EHIP, "sl_write_ply_device: device formatting or copy failed");
+  return io_ok ? SL_OK : SL_EIO;
 }
 
 // Binary little-endian PLY with the reference header's properties (float

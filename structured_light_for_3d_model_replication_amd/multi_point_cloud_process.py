@@ -126,7 +126,7 @@ def process_views(views, calib_data, *, n_cols=1920, n_rows=1080, device=None, w
 
 def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slots, keep, mask_mode="fixed",
                       raise_errors=False, *, xyz_dtype=torch.float64, poses=None, device_sink=None, host=True,
-                      gui_log=False):
+                      gui_log=False, device_ply=False):
     """Views grouped by (frame size, file count), each group through one
     ``pipeline.ViewPipeline``.  ``raise_errors``: a failing folder raises
     (SLSystem.generate_clouds) instead of being logged and skipped (the batch
@@ -139,7 +139,11 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
 
     ``gui_log`` (SLSystem.generate_clouds): each view's lines are
     generate_cloud's (sl_system.py:574-694: decoding, "Processing N valid
-    pixels...", saving, success) instead of the batch GUI's "Saved: ..." line."""
+    pixels...", saving, success) instead of the batch GUI's "Saved: ..." line.
+
+    ``device_ply`` (with ``write`` and not ``keep``): each view's PLY is
+    formatted on the GPU from the points in HBM (ply.save_ply_device, on the
+    pipeline's D2H thread and stream) -- no D2H of the points."""
     files = {f: io.list_stack_files(f) for f in views}
     groups: dict = {}
     for f in views:
@@ -199,8 +203,25 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
             if group[i] not in failed:
                 device_sink(group[i], xyz, bgr)
 
+        def on_device_ply(i, xyz, bgr, group=group, pipe=pipe):
+            f = group[i]
+            if f in failed:
+                return
+            path = os.path.join(f, os.path.basename(f) + ".ply")
+            if gui_log:
+                for line in ("Decoding Columns...", "Decoding Rows...", "Reconstructing 3D points...",
+                             f"Processing {pipe.masked_count(i)} valid pixels...",
+                             f"Saving {len(xyz)} points to {path}..."):
+                    log(line)
+            ply.save_ply_device(xyz, bgr, path)
+            log(f"[Success] Generated {path}" if gui_log else f"Saved: {os.path.basename(f)}.ply ({len(xyz)} points)")
+            out[f] = ([], [])
+
         gposes = None if poses is None else np.stack([np.asarray(poses[f], np.float64).reshape(4, 4)
                                                       for f in group])
+        if device_ply and write and not keep and device_sink is None:
+            pipe.run(len(group), fill, None, on_device=on_device_ply, poses=gposes)
+            continue
         pipe.run(len(group), fill, consume if host else None,
                  on_device=None if device_sink is None else on_device, poses=gposes)
     return {f: out[f] for f in views if f in out}

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 import numpy as np
 
@@ -60,6 +61,26 @@ def save_ply(points, colors, filename, binary: bool = False) -> None:
     fn = _lib.load().sl_write_ply_binary if binary else _lib.load().sl_write_ply
     _lib.check(fn(os.fsencode(filename), P.ctypes.data, dt, C.ctypes.data, n, _THREADS), None,
                f"cannot write {filename}")
+
+
+_WRITERS: dict = {}  # device -> a context of its own for device-side PLY formatting (its scratch, its lock)
+_WRITERS_LOCK = threading.Lock()
+
+
+def save_ply_device(xyz, bgr, filename, stream=None) -> None:
+    """save_ply of a cloud in GPU memory (torch tensors: xyz (n, 3) float32 /
+    float64, bgr (n, 3) uint8): the text is formatted on the GPU by the same
+    digit code as the host formatter (one thread per point), copied back in
+    chunks and written -- byte-identical to save_ply(xyz.cpu(), bgr.cpu(),
+    filename), without the points' D2H or any host formatting.  A context of
+    its own per device keeps the writer off the decoding contexts' locks."""
+    from . import core
+    with _WRITERS_LOCK:
+        key = str(xyz.device)
+        if key not in _WRITERS:
+            _WRITERS[key] = core.Reconstructor(xyz.device)
+        w = _WRITERS[key]
+    w.write_ply(filename, xyz, bgr, stream)
 
 
 def save_ply_open3d(points, colors, filename, normals=None, binary: bool = True) -> None:

@@ -85,18 +85,9 @@ def _stage(dev, n_up, H, W):
     return _STAGE[key]
 
 
-def decode_and_reconstruct(folder, calib, n_cols=1920, n_rows=1080, *, mask_mode="adaptive", device=None,
-                           xyz_dtype=np.float64, count_valid=False, prepared=None):
-    """gray_decode + reconstruct_point_cloud fused in one GPU pass (what
-    generate_cloud runs).  The whole file list is checked with gray_decode's
-    rules (sl_system.py:515-516, 549-554: ValueError below 4 files,
-    IndexError for a pattern without its inverse), but only the files the
-    cloud reads are decoded -- white, black and the column pairs (24 of 46 for
-    11 + 11 bits): reconstruct_point_cloud uses only col_map (:624-629) -- into
-    pinned buffers kept for the next call, and uploaded from there.
-    ``count_valid``: also return the number of masked-in pixels (the kernels
-    count them: sl_mask_counts_to).  ``prepared``: calibration_key(calib, H,
-    W) when the caller has it (SLSystem.generate_cloud caches it per file)."""
+def _decode_device(folder, calib, n_cols, n_rows, mask_mode, device, xyz_dtype, count_valid, prepared):
+    """decode_and_reconstruct's work, the cloud left on the device -> (xyz,
+    bgr device tensors of the n points, masked-in pixel count or None)."""
     files = io.list_stack_files(folder)
     n_up = pipeline.planes_for_cloud(len(files), n_cols, n_rows)
     H, W = io.frame_size(files[0])
@@ -116,8 +107,25 @@ def decode_and_reconstruct(folder, calib, n_cols=1920, n_rows=1080, *, mask_mode
         eng.sync(s)
     cloud = res["cloud"]
     n = cloud.total()
-    P, C = cloud.xyz[:n].cpu().numpy().astype(np.float64, copy=False), cloud.bgr[:n].cpu().numpy()
-    return (P, C, int(mc.item())) if count_valid else (P, C)
+    return cloud.xyz[:n], cloud.bgr[:n], (int(mc.item()) if count_valid else None)
+
+
+def decode_and_reconstruct(folder, calib, n_cols=1920, n_rows=1080, *, mask_mode="adaptive", device=None,
+                           xyz_dtype=np.float64, count_valid=False, prepared=None):
+    """gray_decode + reconstruct_point_cloud fused in one GPU pass (what
+    generate_cloud runs).  The whole file list is checked with gray_decode's
+    rules (sl_system.py:515-516, 549-554: ValueError below 4 files,
+    IndexError for a pattern without its inverse), but only the files the
+    cloud reads are decoded -- white, black and the column pairs (24 of 46 for
+    11 + 11 bits): reconstruct_point_cloud uses only col_map (:624-629) -- into
+    pinned buffers kept for the next call, and uploaded from there.
+    ``count_valid``: also return the number of masked-in pixels (the kernels
+    count them: sl_mask_counts_to).  ``prepared``: calibration_key(calib, H,
+    W) when the caller has it (SLSystem.generate_cloud caches it per file)."""
+    xyz, bgr, n_valid = _decode_device(folder, calib, n_cols, n_rows, mask_mode, device, xyz_dtype, count_valid,
+                                       prepared)
+    P, C = xyz.cpu().numpy().astype(np.float64, copy=False), bgr.cpu().numpy()
+    return (P, C, n_valid) if count_valid else (P, C)
 
 
 def index_error_stage(n_files: int, n_cols: int = 1920, n_rows: int = 1080):
@@ -174,12 +182,14 @@ class SLSystem:
             if hw not in keys:  # the content key (and pinhole check) of this calibration at this frame size
                 keys[hw] = core.Reconstructor.calibration_key(calib, *hw)
             prepared = keys[hw]
-        points, colors, n_valid = decode_and_reconstruct(scan_dir, calib, device=self.device, count_valid=True,
-                                                         prepared=prepared)
+        xyz, bgr, n_valid = _decode_device(scan_dir, calib, 1920, 1080, "adaptive", self.device, np.float64, True,
+                                           prepared)
         print(f"Processing {n_valid} valid pixels...")
         out_path = os.path.join(scan_dir, os.path.basename(scan_dir) + ".ply")
-        print(f"Saving {len(points)} points to {out_path}...")
-        ply.save_ply(points, colors, out_path)
+        print(f"Saving {xyz.shape[0]} points to {out_path}...")
+        # the text formatted on the GPU from the f64 points in HBM (the same
+        # bytes as ply.save_ply: one digit code), no D2H of the points
+        ply.save_ply_device(xyz, bgr, out_path)
         print(f"[Success] Generated {out_path}")
 
     @staticmethod
@@ -230,5 +240,5 @@ class SLSystem:
             if len(io.list_stack_files(d)) < 4:  # sl_system.py:515-516
                 raise ValueError("Not enough images in folder to decode.")
         mp._process_streamed(scan_dirs, calib, 1920, 1080, self.device, True, print, slots, False,
-                             mask_mode="adaptive", raise_errors=True, gui_log=True)
+                             mask_mode="adaptive", raise_errors=True, gui_log=True, device_ply=True)
         return [os.path.join(d, os.path.basename(d) + ".ply") for d in scan_dirs]
