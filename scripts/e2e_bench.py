@@ -188,6 +188,8 @@ def main():
                 os.remove(os.path.join(f, os.path.basename(f) + ".ply"))
             with contextlib.redirect_stdout(_io.StringIO()):
                 slsys.generate_clouds(folders[:2], calib_file)  # warm: pools, pinned slots
+            for f in folders[:2]:  # the timed run writes new files, as the GUI legs do (no overwrite cost)
+                os.remove(os.path.join(f, os.path.basename(f) + ".ply"))
             t0 = time.perf_counter()
             with contextlib.redirect_stdout(_io.StringIO()):
                 slsys.generate_clouds(folders, calib_file)

@@ -138,13 +138,28 @@ def imread_gray(path: str, out: np.ndarray | None = None) -> np.ndarray:
         return _rgb_to_gray_cv(np.asarray(im.convert("RGB")))
 
 
-def imread_bgr(path: str) -> np.ndarray:
-    """cv2.imread(path) equivalent (uint8 H x W x 3, BGR)."""
+def imread_bgr(path: str, out: np.ndarray | None = None) -> np.ndarray:
+    """cv2.imread(path) equivalent (uint8 H x W x 3, BGR), into ``out`` when
+    given.  A colour file is decoded to RGB and packed as BGR by Pillow's raw
+    packer (one pass in C; the same bytes as reversing the RGB channels)."""
     with Image.open(path) as im:
         if im.mode == "L":
             a = np.asarray(im)
-            return np.repeat(a[:, :, None], 3, axis=2)
-        return np.ascontiguousarray(np.asarray(im.convert("RGB"))[:, :, ::-1])
+            res = np.empty(a.shape + (3,), np.uint8) if out is None else out
+            if res.shape != a.shape + (3,):
+                raise ValueError(f"{path}: size {a.shape} differs from {tuple(res.shape[:2])}")
+            res[...] = a[:, :, None]
+            return res
+        rgb = im if im.mode == "RGB" else im.convert("RGB")
+        W, H = rgb.size
+        buf = rgb.tobytes("raw", "BGR")
+    a = np.frombuffer(buf, np.uint8).reshape(H, W, 3)
+    if out is None:
+        return a.copy()
+    if out.shape != (H, W, 3):
+        raise ValueError(f"{path}: size {(H, W)} differs from {tuple(out.shape[:2])}")
+    out[...] = a
+    return out
 
 
 def frame_size(path: str) -> tuple[int, int]:
@@ -177,12 +192,15 @@ def _pool(workers: int):
         return _POOLS[workers]
 
 
-def fill_stack(files: list[str], stack_out, tex_out, workers: int | None = None) -> bool:
+def fill_stack(files: list[str], stack_out, tex_out, workers: int | None = None, on_plane=None) -> bool:
     """Decode files[0 : len(stack_out)] as gray straight into ``stack_out``
     (uint8 [n, H, W], e.g. a pinned tensor's numpy view) and file 0 in colour
     into ``tex_out`` [H, W, 3] BGR -- unless file 0 is single-channel, whose
     colour read is the gray plane replicated (cv2.imread): then ``tex_out`` is
-    left untouched and True is returned (the caller may pass no texture)."""
+    left untouched and True is returned (the caller may pass no texture).
+    The colour decode (the longest task: a colour JPEG's RGB decode) starts
+    first, beside the gray ones.  ``on_plane(j)`` is called, on the decoding
+    thread, as soon as plane j is in ``stack_out`` (e.g. to start its upload)."""
     n = len(stack_out)
     workers = default_workers() if workers is None else workers
     if len(files) < n:
@@ -196,17 +214,28 @@ def fill_stack(files: list[str], stack_out, tex_out, workers: int | None = None)
             if a.shape != shape:
                 raise ValueError(f"{files[j]}: size {a.shape} differs from {shape}")
             dst[...] = a
+        if on_plane is not None:
+            on_plane(j)
+
+    def colour():
+        with Image.open(files[0]) as im:
+            if im.mode == "L":
+                return True
+        imread_bgr(files[0], tex_out)
+        return False
 
     if workers > 1 and n > 1:
-        list(_pool(workers).map(one, range(n)))
-    else:
-        for j in range(n):
-            one(j)
-    with Image.open(files[0]) as im:
-        gray = im.mode == "L"
-    if not gray:
-        tex_out[...] = imread_bgr(files[0])
-    return gray
+        pool = _pool(workers)
+        fc = pool.submit(colour)
+        try:
+            list(pool.map(one, range(n)))
+        except BaseException:
+            fc.exception()  # waited for: nothing writes tex_out after the call returns
+            raise
+        return fc.result()
+    for j in range(n):
+        one(j)
+    return colour()
 
 
 def read_stack(folder: str, workers: int | None = None):

@@ -97,9 +97,12 @@ def _decode_device(folder, calib, n_cols, n_rows, mask_mode, device, xyz_dtype, 
     mc = torch.empty(1, dtype=torch.int64, device=eng.device) if count_valid else None
     with _STAGE_LOCK:  # the staging buffers are shared by the calls of this process
         hs, ht, ds, dt = _stage(eng.device, n_up, H, W)
-        gray_tex = io.fill_stack(files, hs.numpy(), ht.numpy())
         s = torch.cuda.current_stream(eng.device)
-        ds.copy_(hs, non_blocking=True)
+
+        def upload(j):  # each plane's H2D starts on the decoding thread as soon as the plane is in place
+            with torch.cuda.stream(s):
+                ds[j].copy_(hs[j], non_blocking=True)
+        gray_tex = io.fill_stack(files, hs.numpy(), ht.numpy(), on_plane=upload)
         if not gray_tex:
             dt.copy_(ht, non_blocking=True)
         res = eng.decode_triangulate(ds, n_cols, n_rows, texture=None if gray_tex else dt, mask_mode=mask_mode,
@@ -118,7 +121,8 @@ def decode_and_reconstruct(folder, calib, n_cols=1920, n_rows=1080, *, mask_mode
     IndexError for a pattern without its inverse), but only the files the
     cloud reads are decoded -- white, black and the column pairs (24 of 46 for
     11 + 11 bits): reconstruct_point_cloud uses only col_map (:624-629) -- into
-    pinned buffers kept for the next call, and uploaded from there.
+    pinned buffers kept for the next call, each plane uploaded from there
+    as soon as it is decoded (the uploads overlap the remaining decodes).
     ``count_valid``: also return the number of masked-in pixels (the kernels
     count them: sl_mask_counts_to).  ``prepared``: calibration_key(calib, H,
     W) when the caller has it (SLSystem.generate_cloud caches it per file)."""

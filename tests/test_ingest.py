@@ -84,3 +84,54 @@ def test_fill_stack_reads_bmps_in_place(tmp_path):
     bad = np.zeros((6, 9, 12), np.uint8)
     with pytest.raises(ValueError):
         io.fill_stack(files, bad, tex)
+
+
+@pytest.mark.parametrize("fmt,mode", [("PNG", "RGB"), ("JPEG", "RGB"), ("PNG", "P"), ("PNG", "RGBA"), ("BMP", "RGB")])
+def test_imread_bgr_is_the_reversed_rgb_decode(tmp_path, fmt, mode):
+    """imread_bgr packs BGR with Pillow's raw packer: the same bytes as the RGB
+    decode with its channels reversed (what cv2.imread(f) returns for these
+    payloads), returned or written into ``out``."""
+    rng = np.random.default_rng(11)
+    H, W = 17, 29
+    if mode == "P":
+        im = Image.fromarray(rng.integers(0, 256, (H, W), dtype=np.uint8), "P")
+        im.putpalette(rng.integers(0, 256, 768, dtype=np.uint8).tolist())
+    else:
+        im = Image.fromarray(rng.integers(0, 256, (H, W, len(mode)), dtype=np.uint8), mode)
+    f = str(tmp_path / f"c.{fmt.lower()}")
+    im.save(f, format=fmt)
+    with Image.open(f) as j:
+        want = np.asarray(j.convert("RGB"))[:, :, ::-1]
+    np.testing.assert_array_equal(io.imread_bgr(f), want)
+    out = np.zeros((H, W, 3), np.uint8)
+    assert io.imread_bgr(f, out) is out
+    np.testing.assert_array_equal(out, want)
+    with pytest.raises(ValueError):
+        io.imread_bgr(f, np.zeros((H, W + 1, 3), np.uint8))
+
+
+@pytest.mark.parametrize("workers", [1, 4])
+def test_fill_stack_colour_file_and_plane_callback(tmp_path, workers):
+    """A colour file 0 (JPEG bytes under a .bmp name, server/server.py:70):
+    its BGR read lands in tex_out (decoded beside the gray planes), False is
+    returned, and on_plane is called once per plane, after the plane is in
+    place."""
+    rng = np.random.default_rng(3)
+    H, W, n = 12, 20, 5
+    files = []
+    for i in range(n):
+        f = str(tmp_path / f"{i:02d}.bmp")
+        Image.fromarray(rng.integers(0, 256, (H, W, 3), dtype=np.uint8), "RGB").save(f, format="JPEG")
+        files.append(f)
+    st = np.zeros((n, H, W), np.uint8)
+    tex = np.zeros((H, W, 3), np.uint8)
+    seen = {}
+
+    def on_plane(j):
+        seen[j] = st[j].copy()
+    assert io.fill_stack(files, st, tex, workers=workers, on_plane=on_plane) is False
+    for j, f in enumerate(files):
+        np.testing.assert_array_equal(st[j], io.imread_gray(f))
+        np.testing.assert_array_equal(seen[j], st[j])
+    np.testing.assert_array_equal(tex, io.imread_bgr(files[0]))
+    assert sorted(seen) == list(range(n))
