@@ -66,7 +66,8 @@ CONFIGS = {
     # 360-view scan over 8 GPUs (24.8 / 17.2 GB of stacks resident in HBM);
     # c3: the 36-view turntable scan (strong scaling shards it).
     "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0,
-               streams=3,  # with next-stats (2 launches per call): 3 lanes best
+               streams=4, lane_priority=-1,  # 4 lanes on high-priority streams, each with a hardware queue of
+                                             # its own (normal-priority lanes share 2 of the 4 queues)
                ring_control=12),  # the control window's distinct views: 12 x 23 MB > the 256 MiB Infinity Cache
     "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0,
                ring=3, streams=2),  # distinct resident views cycled (no Infinity-Cache
@@ -111,6 +112,8 @@ def parse(argv=None):
                     help="default per config (CONFIGS: measured best, DESIGN.md 6.2); views in flight per GPU: "
                          "successive steps round-robin over this many contexts, each on its own HIP stream "
                          "with its own outputs (one step's kernels overlap the next one's on the other stream)")
+    ap.add_argument("--lane-priority", dest="lane_priority", type=int, default=None,
+                    help="HIP stream priority of the lanes (default per config)")
     ap.add_argument("--gather", default="torch", choices=["torch", "native"],
                     help="N > 1: the cloud gather through torch.distributed's RCCL communicator, or the "
                          "library's own (sl_gather_init / sl_gather_counts / sl_gather)")
@@ -708,9 +711,10 @@ def main():
     # outputs) on one HIP stream each; step i runs on lane i % S.  S = 1: the
     # plain engine on the current stream
     S = max(1, a.streams if a.streams is not None else cfg.get("streams", 1))
+    lane_prio = a.lane_priority if a.lane_priority is not None else cfg.get("lane_priority", 0)
     pool = None
     if S > 1:
-        pool = core.ReconstructorPool(dev, lanes=S, reuse_outputs=True)
+        pool = core.ReconstructorPool(dev, lanes=S, reuse_outputs=True, stream_priority=lane_prio)
         pool.set_calibration(calib, H, W)
         pool.reserve(V, H * W)
         eng = pool.engines[0]
@@ -1124,6 +1128,7 @@ def main():
                                       if ring_R > 1 else ""),
                        "views_per_gpu": V, "views_total": V_total, "H": H, "W": W, "projector": f"{Wp}x{Hp}",
                        "parallelism": f"views sharded over {world} GPU(s)", "streams_per_gpu": S,
+                       "lane_stream_priority": lane_prio if S > 1 else None,
                        "next_stats": bool(a.next_stats)},
             "timing": {"preroll": pre,
                        "step_us": spread(step_us),

@@ -571,14 +571,21 @@ class ReconstructorPool:
     that the inputs are ready AND, with ``reuse_outputs``, that nothing still
     queued on another stream reads the lane's previous outputs (e.g. it never
     reads them, or it synchronised after reading them) -- the lane's kernels
-    would otherwise overwrite results a queued reader has not consumed."""
+    would otherwise overwrite results a queued reader has not consumed.
 
-    def __init__(self, device=None, lanes: int = 2, reuse_outputs: bool = False):
+    ``stream_priority``: the lanes' HIP stream priority.  Lanes run
+    concurrently only on different hardware queues; on this runtime
+    normal-priority streams share 4 (the third lane of a pool lands on the
+    second's, measured in rocprofv3 traces: profiles/r06_c1/queues.jsonl),
+    while each high-priority stream (-1) got one of its own -- config 1 with 3
+    lanes 18.9-19.4 -> 14.7-15.1 us per view."""
+
+    def __init__(self, device=None, lanes: int = 2, reuse_outputs: bool = False, stream_priority: int = 0):
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
         self.engines = [Reconstructor(device) for _ in range(lanes)]
         self.device = self.engines[0].device
-        self.streams = [torch.cuda.Stream(self.device) for _ in range(lanes)]
+        self.streams = [torch.cuda.Stream(self.device, priority=stream_priority) for _ in range(lanes)]
         self._outs = [{} if reuse_outputs else None for _ in range(lanes)]
         self._keys = [None] * lanes  # a lane's last output shapes (reused buffers: no allocation)
         self._plans = [{} for _ in range(lanes)]  # a lane's prepared calls by argument key (resident inputs)
