@@ -68,6 +68,7 @@ CONFIGS = {
     "c1": dict(H=720, W=1280, Wp=1024, Hp=768, rows=False, views=1, maps=True, pose=False, deg=10.0,
                streams=4, lane_priority=-1,  # 4 lanes on high-priority streams, each with a hardware queue of
                                              # its own (normal-priority lanes share 2 of the 4 queues)
+               steps=200,  # 20 steps of ~11 us: 14 us per step measured, the lanes' fill and drain
                ring_control=12),  # the control window's distinct views: 12 x 23 MB > the 256 MiB Infinity Cache
     "c2": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=1, maps=True, pose=False, deg=10.0,
                ring=3, streams=2),  # distinct resident views cycled (no Infinity-Cache
@@ -97,7 +98,9 @@ def parse(argv=None):
                     help="process-group backend (gloo only with --selftest)")
     ap.add_argument("--selftest", action="store_true",
                     help="CPU plumbing test of the launcher / timing / gather (no GPU, no kernels)")
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default per config: 20; c1 200 -- its 11-us steps on 4 lanes would otherwise "
+                         "leave a quarter of a 20-step window to the lanes' fill and drain)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--preroll-ms", dest="preroll_ms", type=float, default=300.0,
                     help="untimed back-to-back steps after the warm-up, before the timed window (ms)")
@@ -157,7 +160,10 @@ def parse(argv=None):
     ap.add_argument("--traffic", default=None,
                     help="PMC-derived HBM bytes per step (committed profile of the same workload, "
                          "scripts/traffic_from_pmc.py); default " + TRAFFIC_DIR + "/traffic_<config>.json")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.steps is None:
+        a.steps = CONFIGS[a.config].get("steps", 20)
+    return a
 
 
 def _free_port() -> int:

@@ -2358,14 +2358,31 @@ int bit_count(int n) {  // int(np.ceil(np.log2(n))) for n >= 1
   return b;
 }
 
+int zero_async(sl_ctx* c, void* p, int64_t words, hipStream_t s);
+
+// *ptr grown to at least `need` elements (at least twice the old capacity),
+// zeroed: on stream s when on_stream -- a kernel ordered before the work the
+// caller enqueues there next -- else before returning.  (A bare hipMemset
+// runs on the null stream, which non-blocking streams -- torch's pool
+// streams, ReconstructorPool's lanes -- do not wait for: a call's first
+// kernels could overtake the zeroing of the scratch they accumulate into.
+// Seen as a wrong adaptive mask on a lane once the lanes had hardware queues
+// of their own, tests/test_gpu_pool.py.)
 template <typename T>
-int grow(sl_ctx* c, T** ptr, int64_t* cap, int64_t need) {
+int grow(sl_ctx* c, T** ptr, int64_t* cap, int64_t need, hipStream_t s = nullptr, bool on_stream = false) {
   if (need <= *cap) return SL_OK;
   if (*ptr) HIP_TRY(c, hipFree(*ptr));
   *ptr = nullptr;
   const int64_t n = std::max<int64_t>(need, *cap * 2);
-  HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(ptr), sizeof(T) * n));
-  HIP_TRY(c, hipMemset(*ptr, 0, sizeof(T) * n));
+  const int64_t words = (static_cast<int64_t>(sizeof(T)) * n + 3) / 4;
+  HIP_TRY(c, hipMalloc(reinterpret_cast<void**>(ptr), 4 * words));
+  if (on_stream) {
+    const int r = zero_async(c, *ptr, words, s);
+    if (r) return r;
+  } else {
+    HIP_TRY(c, hipMemset(*ptr, 0, 4 * words));
+    HIP_TRY(c, hipDeviceSynchronize());
+  }
   *cap = n;
   return SL_OK;
 }
@@ -2374,21 +2391,22 @@ int grow(sl_ctx* c, T** ptr, int64_t* cap, int64_t need) {
 // max(views, hist_views)); *hist_fresh: the histogram buffer was
 // (re)allocated (zeroed: a pass queued in it is gone)
 int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes, int64_t hist_views = 0,
-                   bool* hist_fresh = nullptr) {
+                   bool* hist_fresh = nullptr, hipStream_t s = nullptr, bool on_stream = false) {
   const int64_t chunks = views * ((px + kChunk - 1) / kChunk);
-  int r = grow(c, &c->d_chunk_counts, &c->cap_cc, chunks);
+  int r = grow(c, &c->d_chunk_counts, &c->cap_cc, chunks, s, on_stream);
   if (r) return r;
-  r = grow(c, &c->d_block_sums, &c->cap_bs, views * (((px + kChunk - 1) / kChunk + kWaves - 1) / kWaves));
+  r = grow(c, &c->d_block_sums, &c->cap_bs, views * (((px + kChunk - 1) / kChunk + kWaves - 1) / kWaves), s,
+           on_stream);
   if (r) return r;
-  r = grow(c, &c->d_ptnib, &c->cap_ptnib, chunks * kChunkNib);
+  r = grow(c, &c->d_ptnib, &c->cap_ptnib, chunks * kChunkNib, s, on_stream);
   if (r) return r;
   int64_t scap = c->d_super ? kSuperWords : 0;
-  r = grow(c, &c->d_super, &scap, kSuperWords);  // zeroed once; then by the kernels (super_produce)
+  r = grow(c, &c->d_super, &scap, kSuperWords, s, on_stream);  // zeroed once; then by the kernels (super_produce)
   if (r) return r;
   const int64_t before = c->cap_hist, need = std::max(views, hist_views) * kHistView;
   for (int d = 0; d < 2; ++d) {  // k_stats' replicas (k_decode's: kSlot)
     int64_t cap = before;
-    r = grow(c, &c->d_hist[d], &cap, need);
+    r = grow(c, &c->d_hist[d], &cap, need, s, on_stream);
     if (r) return r;
     if (d == 1) c->cap_hist = cap;
   }
@@ -2400,7 +2418,8 @@ int ensure_scratch(sl_ctx* c, int64_t views, int64_t px, bool codes, int64_t his
   // (u16 units: 2 B/px, or the 1536-B slots of whole chunk groups)
   if (codes)
     return grow(c, &c->d_codes, &c->cap_codes,
-                std::max<int64_t>(views * px, views * ((px + 4 * kChunk - 1) / (4 * kChunk)) * 4 * (kRecSlot / 2)) + 16);
+                std::max<int64_t>(views * px, views * ((px + 4 * kChunk - 1) / (4 * kChunk)) * 4 * (kRecSlot / 2)) + 16,
+                s, on_stream);
   return SL_OK;
 }
 
@@ -2519,9 +2538,9 @@ int launch_groups(sl_ctx* c, const Params& p0, bool vec, int decode_mode, int co
   const bool pre_run = arms.decl && cloud_mode >= 0 && vec;
   bool hist_fresh = false;
   int r = ensure_scratch(c, std::min(vpg, p0.n_views), p0.HW, codes, pre_run ? std::min(vpg, c->decl_views) : 0,
-                         &hist_fresh);
+                         &hist_fresh, s, true);
   if (r) return r;
-  r = grow(c, &c->d_stats, &c->cap_stats, p0.n_views);
+  r = grow(c, &c->d_stats, &c->cap_stats, p0.n_views, s, true);
   if (r) return r;
   unsigned long long cap_id = 0;
   r = capture_of(c, s, &cap_id);
@@ -3776,9 +3795,9 @@ int sl_write_ply_device(sl_ctx* c, const char* path, const void* xyz, int xyz_dt
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t nb = std::max<int64_t>(1, (n + kPlyBlock - 1) / kPlyBlock);
-  int r = grow(c, &c->d_ply_bsum, &c->cap_ply_bsum, nb + 1);  // [nb]: the fallback flag
+  int r = grow(c, &c->d_ply_bsum, &c->cap_ply_bsum, nb + 1, s, true);  // [nb]: the fallback flag
   if (r) return r;
-  r = grow(c, &c->d_ply_boff, &c->cap_ply_boff, nb + 1);
+  r = grow(c, &c->d_ply_boff, &c->cap_ply_boff, nb + 1, s, true);
   if (r) return r;
   unsigned* flag = c->d_ply_bsum + nb;
   r = zero_async(c, flag, 1, s);
@@ -3810,7 +3829,7 @@ int sl_write_ply_device(sl_ctx* c, const char* path, const void* xyz, int xyz_dt
     HIP_TRY(c, hipStreamSynchronize(s));
     return sl_write_ply(path, hx.data(), xyz_dtype, hb.data(), n, 16);
   }
-  r = grow(c, &c->d_ply_text, &c->cap_ply_text, std::max<int64_t>(total, 1));
+  r = grow(c, &c->d_ply_text, &c->cap_ply_text, std::max<int64_t>(total, 1), s, true);
   if (r) return r;
   if (n > 0) {
     if (f64)

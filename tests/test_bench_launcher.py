@@ -77,6 +77,9 @@ def test_streams_defaults_per_config():
     assert bench.CONFIGS["c1"]["streams"] == 4 and bench.CONFIGS["c5"]["streams"] == 2
     # c1's lanes on high-priority streams (a hardware queue each), the others at the default
     assert bench.CONFIGS["c1"]["lane_priority"] == -1 and bench.parse([]).lane_priority is None
+    # timed steps: 20 (the driver's command passes --steps itself), c1 200 (its window's fill and drain)
+    assert bench.parse([]).steps == 20 and bench.parse(["--config", "c1"]).steps == 200
+    assert bench.parse(["--config", "c1", "--steps", "20"]).steps == 20
     assert all("lane_priority" not in bench.CONFIGS[c] for c in ("c2", "c3", "c4", "c5"))
     assert bench.CONFIGS["c3"]["streams"] == 2 and bench.CONFIGS["c4"]["streams"] == 2  # measured, DESIGN 5.2
     # c2: two lanes over a ring of distinct resident views (round 5: 2 lanes
