@@ -76,9 +76,9 @@ CONFIGS = {
     "c3": dict(H=1080, W=1920, Wp=1920, Hp=1080, rows=True, views=36, maps=False, pose=False, deg=10.0,
                streams=2),
     "c4": dict(H=3000, W=4000, Wp=1920, Hp=1080, rows=True, views=45, maps=False, pose=False, deg=1.0,
-               streams=2),
+               streams=3, lane_priority=-1),  # 3 lanes, a hardware queue each
     "c5": dict(H=2160, W=3840, Wp=1920, Hp=1080, rows=True, views=45, maps=False, pose=True, deg=1.0,
-               streams=2),
+               streams=3, lane_priority=-1),
 }
 
 

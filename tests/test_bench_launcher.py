@@ -74,14 +74,15 @@ def test_streams_defaults_per_config():
     import bench
     assert bench.parse([]).streams is None
     assert bench.parse(["--streams", "3"]).streams == 3
-    assert bench.CONFIGS["c1"]["streams"] == 4 and bench.CONFIGS["c5"]["streams"] == 2
+    assert bench.CONFIGS["c1"]["streams"] == 4 and bench.CONFIGS["c5"]["streams"] == 3
     # c1's lanes on high-priority streams (a hardware queue each), the others at the default
     assert bench.CONFIGS["c1"]["lane_priority"] == -1 and bench.parse([]).lane_priority is None
     # timed steps: 20 (the driver's command passes --steps itself), c1 200 (its window's fill and drain)
     assert bench.parse([]).steps == 20 and bench.parse(["--config", "c1"]).steps == 200
     assert bench.parse(["--config", "c1", "--steps", "20"]).steps == 20
-    assert all("lane_priority" not in bench.CONFIGS[c] for c in ("c2", "c3", "c4", "c5"))
-    assert bench.CONFIGS["c3"]["streams"] == 2 and bench.CONFIGS["c4"]["streams"] == 2  # measured, DESIGN 5.2
+    assert all(bench.CONFIGS[c]["lane_priority"] == -1 for c in ("c4", "c5"))  # 3 lanes need 3 queues
+    assert all("lane_priority" not in bench.CONFIGS[c] for c in ("c2", "c3"))
+    assert bench.CONFIGS["c3"]["streams"] == 2 and bench.CONFIGS["c4"]["streams"] == 3  # measured, DESIGN 5.2 / 6.2
     # c2: two lanes over a ring of distinct resident views (round 5: 2 lanes
     # 114 vs 121 us per step once the maps and xyz left with nt stores)
     assert bench.CONFIGS["c2"]["streams"] == 2 and bench.CONFIGS["c2"]["ring"] == 3
