@@ -717,7 +717,8 @@ def main():
     # outputs) on one HIP stream each; step i runs on lane i % S.  S = 1: the
     # plain engine on the current stream
     S = max(1, a.streams if a.streams is not None else cfg.get("streams", 1))
-    lane_prio = a.lane_priority if a.lane_priority is not None else cfg.get("lane_priority", 0)
+    lane_prio = a.lane_priority if a.lane_priority is not None else cfg.get("lane_priority", 0)  # (explicit: the
+    # pool's own default would give configs 3 lanes or more high priority as well)
     pool = None
     if S > 1:
         pool = core.ReconstructorPool(dev, lanes=S, reuse_outputs=True, stream_priority=lane_prio)

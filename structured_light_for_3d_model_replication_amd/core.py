@@ -584,16 +584,19 @@ class ReconstructorPool:
     reads them, or it synchronised after reading them) -- the lane's kernels
     would otherwise overwrite results a queued reader has not consumed.
 
-    ``stream_priority``: the lanes' HIP stream priority.  Lanes run
-    concurrently only on different hardware queues; on this runtime
-    normal-priority streams share 4 (the third lane of a pool lands on the
-    second's, measured in rocprofv3 traces: profiles/r06_c1/queues.jsonl),
-    while each high-priority stream (-1) got one of its own -- config 1 with 3
-    lanes 18.9-19.4 -> 14.7-15.1 us per view."""
+    ``stream_priority``: the lanes' HIP stream priority (default: high, -1,
+    for more than 2 lanes, else normal, 0).  Lanes run concurrently only on
+    different hardware queues; on this runtime normal-priority streams share 4
+    (the third lane of a pool lands on the second's, measured in rocprofv3
+    traces: profiles/r06_c1/queues.jsonl), while each high-priority stream got
+    one of its own -- config 1 with 3 lanes 18.9-19.4 -> 14.7-15.1 us per view
+    (DESIGN.md 6.2)."""
 
-    def __init__(self, device=None, lanes: int = 2, reuse_outputs: bool = False, stream_priority: int = 0):
+    def __init__(self, device=None, lanes: int = 2, reuse_outputs: bool = False, stream_priority: int | None = None):
         if lanes < 1:
             raise ValueError("lanes must be >= 1")
+        if stream_priority is None:
+            stream_priority = -1 if lanes > 2 else 0
         self.engines = [Reconstructor(device) for _ in range(lanes)]
         self.device = self.engines[0].device
         self.streams = [torch.cuda.Stream(self.device, priority=stream_priority) for _ in range(lanes)]

@@ -343,3 +343,17 @@ def test_pool_explicit_out_is_not_kept_unless_prepared():
         np.testing.assert_array_equal(a, b)
     pool.close()
     eng.close()
+
+
+def test_pool_default_stream_priority():
+    """More than two lanes get high-priority streams by default (a hardware
+    queue each on this runtime); one or two keep the normal."""
+    from structured_light_for_3d_model_replication_amd import core
+    dev = torch.device("cuda", 0)
+    for lanes, want in ((1, 0), (2, 0), (3, -1), (4, -1)):
+        pool = core.ReconstructorPool(dev, lanes=lanes)
+        assert [s.priority for s in pool.streams] == [want] * lanes
+        pool.close()
+    pool = core.ReconstructorPool(dev, lanes=3, stream_priority=0)
+    assert [s.priority for s in pool.streams] == [0, 0, 0]
+    pool.close()
