@@ -121,6 +121,13 @@ def read_bmp_gray(path: str, out: np.ndarray | None = None) -> np.ndarray | None
     return out
 
 
+def is_raw_bmp(path: str) -> bool:
+    """An uncompressed BMP that read_bmp_gray reads without a decoder (a
+    copy-bound read), as opposed to PNG / JPEG / RLE payloads (decode-bound)."""
+    with open(path, "rb") as f:
+        return _bmp_layout(f.read(14 + 124 + 1024)) is not None
+
+
 def imread_gray(path: str, out: np.ndarray | None = None) -> np.ndarray:
     """cv2.imread(path, 0) equivalent (uint8 H x W)."""
     a = read_bmp_gray(path, out)

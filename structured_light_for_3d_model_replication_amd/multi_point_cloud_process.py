@@ -171,9 +171,12 @@ def _process_streamed(views, calib_data, n_cols, n_rows, device, write, log, slo
 
         def fill(i, stack, tex, group=group):
             try:
-                # half the core share: the D2H thread formats the previous views' PLY files meanwhile
-                return io.fill_stack(files[group[i]], stack.numpy(), tex.numpy(),
-                                     workers=max(1, io.default_workers() // 2))
+                # raw BMPs (copy-bound): half the core share, the D2H thread writes the previous
+                # views' PLY files meanwhile; PNG / JPEG payloads (decode-bound): the whole share
+                fl = files[group[i]]
+                share = io.default_workers()
+                return io.fill_stack(fl, stack.numpy(), tex.numpy(),
+                                     workers=max(1, share // 2) if io.is_raw_bmp(fl[0]) else share)
             except (OSError, ValueError) as e:
                 if raise_errors:
                     raise

@@ -135,3 +135,12 @@ def test_fill_stack_colour_file_and_plane_callback(tmp_path, workers):
         np.testing.assert_array_equal(seen[j], st[j])
     np.testing.assert_array_equal(tex, io.imread_bgr(files[0]))
     assert sorted(seen) == list(range(n))
+
+
+def test_is_raw_bmp(tmp_path):
+    a = np.random.default_rng(4).integers(0, 256, (6, 8), dtype=np.uint8)
+    Image.fromarray(a).save(str(tmp_path / "raw.bmp"))
+    Image.fromarray(a).save(str(tmp_path / "jpeg.bmp"), format="JPEG")  # server/server.py:70
+    Image.fromarray(a).save(str(tmp_path / "x.png"))
+    assert io.is_raw_bmp(str(tmp_path / "raw.bmp"))
+    assert not io.is_raw_bmp(str(tmp_path / "jpeg.bmp")) and not io.is_raw_bmp(str(tmp_path / "x.png"))
