@@ -172,3 +172,40 @@ def test_open3d_layout_writer_round_trip(tmp_path, binary):
         np.testing.assert_allclose(N2, N, rtol=1e-5, atol=1e-5)
     ply.save_ply_open3d(P, C, f)
     assert ply.read_normals(f) is None
+
+
+def test_writer_replaces_large_files_and_keeps_links(tmp_path):
+    """A large regular file already at the path (a re-run over the same scan)
+    is replaced -- renamed away and unlinked beside the write -- with the
+    same bytes as a fresh write and the old file's mode; no side file stays
+    behind.  Symlinks are written through and hard-linked files truncated in
+    place, as open(path, 'w') does."""
+    import stat
+    import time
+    rng = np.random.default_rng(8)
+    n = 200_000
+    P = rng.standard_normal((n, 3)) * 100
+    C = rng.integers(0, 256, (n, 3), dtype=np.uint8)
+    want = ply.ply_text(P, C).encode()
+    f = tmp_path / "scan.ply"
+    f.write_bytes(b"x" * (20 << 20))
+    os.chmod(f, 0o640)
+    ply.save_ply(P, C, str(f))
+    assert f.read_bytes() == want and stat.S_IMODE(os.stat(f).st_mode) == 0o640
+    for _ in range(100):  # the old file's unlink runs on another thread
+        if sorted(p.name for p in tmp_path.iterdir()) == ["scan.ply"]:
+            break
+        time.sleep(0.05)
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["scan.ply"]
+    # a symlink: the target is written, the link stays a link
+    tgt = tmp_path / "target.ply"
+    tgt.write_bytes(b"y" * (20 << 20))
+    lnk = tmp_path / "link.ply"
+    lnk.symlink_to(tgt)
+    ply.save_ply(P[:10], C[:10], str(lnk))
+    assert lnk.is_symlink() and tgt.read_bytes() == ply.ply_text(P[:10], C[:10]).encode()
+    # a hard-linked file: both names see the new bytes
+    h2 = tmp_path / "hard2.ply"
+    os.link(tgt, h2)
+    ply.save_ply(P, C, str(tgt))
+    assert h2.read_bytes() == want and os.stat(tgt).st_ino == os.stat(h2).st_ino
