@@ -248,7 +248,11 @@ int sl_time_kernels(sl_ctx* ctx, int reps, double* decode_ms, double* count_ms, 
  * sl_format_ply: with out == NULL only *out_len is set (the byte size). */
 int sl_format_ply(const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n, int threads, char* out,
                   int64_t out_capacity, int64_t* out_len);
-/* Write that text to `path` (replaces save_ply, sl_system.py:665-691). */
+/* Write that text to `path` (replaces save_ply, sl_system.py:665-691).  A
+ * large regular file already at `path` is renamed away and unlinked beside the
+ * write rather than truncated in place (the same file results, faster);
+ * symlinks and hard-linked files are written through / truncated as
+ * open(path, "w") does.  The same for sl_write_ply_device / _binary. */
 int sl_write_ply(const char* path, const void* xyz, int xyz_dtype, const uint8_t* bgr, int64_t n, int threads);
 
 /* The same file from a cloud in device memory (xyz / bgr device pointers,
