@@ -3065,7 +3065,9 @@ struct PlyReaper {
   std::condition_variable cv;
   int pending = 0;
   unsigned long seq = 0;
+  const pid_t owner = getpid();  // (a forked child has none of the unlink threads: it does not wait)
   ~PlyReaper() {
+    if (getpid() != owner) return;
     std::unique_lock<std::mutex> lk(m);
     cv.wait_for(lk, std::chrono::seconds(10), [this] { return pending == 0; });
   }
