@@ -203,3 +203,42 @@ def test_generate_clouds_prints_generate_clouds_lines(tmp_path, capsys):
     assert want and out.count(want[0]) == 2
     for f in dirs:
         assert f"[Success] Generated {f}/{os.path.basename(f)}.ply" in out
+
+
+def test_generate_cloud_colour_jpeg_capture(tmp_path):
+    """A colour capture as the Android app uploads it -- JPEG bytes under .bmp
+    names (server/server.py:70): generate_cloud (the colour file decoded
+    beside the gray planes, each plane uploaded as it lands) and the batched
+    generate_clouds (the whole decode share for such payloads) write the PLY
+    the oracle writes from the same decoded planes and texture.  (Parity with
+    cv2's own JPEG decoder is unpinned: cv2 is not in this image.)"""
+    from oracle import sl_oracle as o
+    from structured_light_for_3d_model_replication_amd import io
+    from structured_light_for_3d_model_replication_amd.sl_system import SLSystem
+    d = g.load("sl_generate_cloud_e2e")
+    mat = str(tmp_path / "calib.mat")
+    scipy.io.savemat(mat, d["calib"])
+    scans = []
+    for k in range(2):
+        scan = tmp_path / f"jpg_{k}"
+        os.makedirs(scan)
+        for i, im in enumerate(d["stack"]):
+            a = np.ascontiguousarray(im).astype(np.int16)
+            rgb = np.stack([a, np.clip(a - 9 * k, 0, 255), np.clip(a * 7 // 8 + 3, 0, 255)], -1).astype(np.uint8)
+            Image.fromarray(rgb, "RGB").save(str(scan / f"{i + 1:02d}.bmp"), format="JPEG", quality=92)
+        scans.append(str(scan))
+    want = []
+    for scan in scans:
+        files = io.list_stack_files(scan)
+        assert not io.is_raw_bmp(files[0])
+        planes = [io.imread_gray(f) for f in files]
+        P, C = o.decode_triangulate(planes, io.imread_bgr(files[0]), d["calib"], 1920, 1080)[3:]
+        assert len(P) > 1000
+        want.append(o.ply_text(P, C))
+    for scan, w in zip(scans, want):
+        SLSystem().generate_cloud(scan, mat)
+        assert open(os.path.join(scan, os.path.basename(scan) + ".ply")).read() == w
+        os.remove(os.path.join(scan, os.path.basename(scan) + ".ply"))
+    SLSystem().generate_clouds(scans, mat)
+    for scan, w in zip(scans, want):
+        assert open(os.path.join(scan, os.path.basename(scan) + ".ply")).read() == w
