@@ -73,3 +73,27 @@ def test_device_ply_of_a_decoded_cloud(tmp_path):
         ply.save_ply_device(cl.xyz[:n], cl.bgr[:n], str(out))
         assert out.read_bytes() == ply.ply_text(cl.xyz[:n].cpu().numpy(), cl.bgr[:n].cpu().numpy()).encode()
     eng.close()
+
+
+def test_device_ply_replaces_an_existing_file(tmp_path):
+    """A re-run over the same scan: the PLY already there (large, so the
+    writer renames it away and unlinks it beside the write) is replaced by
+    the same bytes a new file gets, its mode kept, no side file left."""
+    import os
+    import stat
+    import time
+    from structured_light_for_3d_model_replication_amd import ply
+    rng = np.random.default_rng(21)
+    xyz = rng.standard_normal((50_000, 3)) * 50
+    bgr = rng.integers(0, 256, (50_000, 3), dtype=np.uint8)
+    out = tmp_path / "scan.ply"
+    out.write_bytes(b"z" * (24 << 20))
+    os.chmod(out, 0o600)
+    ply.save_ply_device(torch.from_numpy(xyz).cuda(), torch.from_numpy(bgr).cuda(), str(out))
+    assert out.read_bytes() == ply.ply_text(xyz, bgr).encode()
+    assert stat.S_IMODE(os.stat(out).st_mode) == 0o600
+    for _ in range(100):
+        if [p.name for p in tmp_path.iterdir()] == ["scan.ply"]:
+            break
+        time.sleep(0.05)
+    assert [p.name for p in tmp_path.iterdir()] == ["scan.ply"]
