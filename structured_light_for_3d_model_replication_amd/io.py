@@ -81,6 +81,9 @@ def _bmp_layout(head: bytes):
     return off, abs(H), W, bpp, H > 0, pal
 
 
+_TLS = threading.local()  # per decoding thread: a reused read buffer
+
+
 def read_bmp_gray(path: str, out: np.ndarray | None = None) -> np.ndarray | None:
     """cv2.imread(path, 0) of an uncompressed BMP without a full decode:
     8-bit (palette mapped; gray palettes are the identity), 24/32-bit BGR(x)
@@ -96,11 +99,24 @@ def read_bmp_gray(path: str, out: np.ndarray | None = None) -> np.ndarray | None
         bpr = W * bpp // 8
         stride = (bpr + 3) & ~3
         f.seek(off)
-        raw = f.read(stride * H)
-    if len(raw) < stride * H - (stride - bpr):
+        # into this thread's reused buffer: a fresh 8-MB bytes object per file would be
+        # page-faulted in (and zeroed) by the kernel every time
+        need = stride * H
+        buf = getattr(_TLS, "buf", None)
+        if buf is None or len(buf) < need:
+            buf = _TLS.buf = bytearray(need)
+        mv = memoryview(buf)[:need]
+        got = 0
+        while got < need:
+            k = f.readinto(mv[got:])
+            if not k:
+                break
+            got += k
+    if got < need - (stride - bpr):
         raise ValueError(f"{path}: truncated BMP pixel array")
-    raw = raw.ljust(stride * H, b"\0")
-    rows = np.frombuffer(raw, np.uint8).reshape(H, stride)[:, :bpr]
+    if got < need:
+        mv[got:] = bytes(need - got)
+    rows = np.frombuffer(buf, np.uint8, need).reshape(H, stride)[:, :bpr]
     if bottom_up:
         rows = rows[::-1]
     if out is None:
